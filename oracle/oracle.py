@@ -1,0 +1,169 @@
+"""ctypes front end of the C oracle (qldpc_oracle.c) — TEST INFRASTRUCTURE ONLY.
+
+Parity pinned against golden vectors from the unmodified reference decoders
+(tests/golden/gen_golden.py -> tests/test_oracle_golden.py).
+The OSD restatement (`osd_dec`) is pure NumPy/Python, small cases only.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libqldpc_oracle.so")
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        P = ctypes.c_void_p
+        L.oracle_decode_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P,
+                                          ctypes.c_int, P, P, P, ctypes.c_long, ctypes.c_double,
+                                          ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                                          P, P, P, P, ctypes.c_int]
+        L.oracle_decode_batch.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def csr(H):
+    H = np.asarray(H)
+    rows, cols = np.nonzero(H)            # row-major == np.where(H) edge order (decoders.py:224)
+    row_ptr = np.zeros(H.shape[0] + 1, np.int32)
+    np.add.at(row_ptr, rows + 1, 1)
+    return np.cumsum(row_ptr, dtype=np.int64).astype(np.int32), cols.astype(np.int32)
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def decode_batch(algo, H, syn, p, max_iter, layer_ptr=None, layer_rows=None, beta=0.75,
+                 eps=1e-9, want_post=True, nthreads=None):
+    """Decode a batch of syndromes (uint8 [B, m]). algo: "MS" | "BP".
+
+    Returns (ehat uint8[B,n], iters int32[B], post f64[B,n] | None, flags int32[B]).
+    """
+    H = np.asarray(H)
+    m, n = H.shape
+    rp, ci = csr(H)
+    if layer_ptr is None:
+        layer_ptr = np.array([0, m], np.int32)
+        layer_rows = np.arange(m, dtype=np.int32)
+    layer_ptr = np.ascontiguousarray(layer_ptr, np.int32)
+    layer_rows = np.ascontiguousarray(layer_rows, np.int32)
+    syn = np.ascontiguousarray(syn, np.uint8).reshape(-1, m)
+    B = syn.shape[0]
+    ehat = np.zeros((B, n), np.uint8)
+    iters = np.zeros(B, np.int32)
+    post = np.zeros((B, n), np.float64) if want_post else None
+    flags = np.zeros(B, np.int32)
+    rc = lib().oracle_decode_batch(0 if algo == "MS" else 1, m, n, _p(rp), _p(ci),
+                                   len(layer_ptr) - 1, _p(layer_ptr), _p(layer_rows), _p(syn), B,
+                                   float(p), int(max_iter), float(beta), float(eps), _p(ehat),
+                                   _p(iters), _p(post), _p(flags),
+                                   int(nthreads or os.cpu_count() or 1))
+    if rc != 0:
+        raise RuntimeError("oracle_decode_batch failed")
+    return ehat, iters, post, flags
+
+
+# --------------------------------------------------------------------------
+# OSD restatement (decoders.py:299-370, gf2math.py:91-187). Small cases only.
+# --------------------------------------------------------------------------
+def gf2_rank(A):
+    """gf2math.rank (gf2math.py:91-135)."""
+    A = (np.asarray(A, dtype=np.uint8) & 1).copy()
+    m, n = A.shape
+    row = 0
+    for col in range(n):
+        piv = None
+        for r in range(row, m):
+            if A[r, col]:
+                piv = r
+                break
+        if piv is None:
+            continue
+        if piv != row:
+            A[[row, piv]] = A[[piv, row]]
+        for r in range(m):
+            if r != row and A[r, col]:
+                A[r] ^= A[row]
+        row += 1
+        if row == m:
+            break
+    return row
+
+
+def gf2_ref_T(A):
+    """Transform T of gf2math.REF(A, reduced=True) (gf2math.py:139-187)."""
+    B = (np.asarray(A) & 1).astype(np.int8).copy()
+    nR, nC = B.shape
+    T = np.identity(nR, dtype=np.int8)
+    x = 0
+    for c in range(nC):
+        r = x
+        while r < nR and B[r, c] == 0:
+            r += 1
+        if r == nR:
+            continue
+        if r != x:
+            B[[x, r]] = B[[r, x]]
+            T[[x, r]] = T[[r, x]]
+        for s in range(r + 1, nR):
+            if B[s, c]:
+                B[s] ^= B[x]
+                T[s] ^= T[x]
+        for s in range(x):
+            if B[s, c]:
+                B[s] ^= B[x]
+                T[s] ^= T[x]
+        x += 1
+        if x >= nR:
+            break
+    return T
+
+
+def osd_dec(H, e_hat, syndrome, post, order=0):
+    """OSDdec restated (decoders.py:299-370), including its aliasing semantics."""
+    H = (np.asarray(H) & 1).astype(np.int64)
+    e_hat = np.asarray(e_hat).copy()
+    post = np.asarray(post, dtype=np.float64)
+    sat = np.where(np.abs(post) < 100.0, post, 100.0 * np.sign(post))
+    prob = 1.0 / (1.0 + np.exp(sat))
+    rel = np.where(prob > 0.5, prob, 1 - prob)
+    perm = np.argsort(rel)
+    Hp = H[:, perm]
+    J = [0]
+    max_rank = gf2_rank(Hp)
+    past = gf2_rank(Hp[:, J])
+    nxt = 1
+    while True:
+        J.append(nxt)
+        new = gf2_rank(Hp[:, J])
+        nxt += 1
+        if new <= past:
+            J.pop()
+            continue
+        if new >= max_rank:
+            break
+        past = new
+    info = list(set(range(H.shape[1])) - set(J))
+    ep = e_hat[perm]
+    T = gf2_ref_T(Hp[:, J])
+    for w in range(2 ** order):
+        flips = np.array([(w >> b) & 1 for b in range(len(info))])
+        ep[info] ^= flips
+        sJ = (np.asarray(syndrome) + Hp[:, info] @ ep[info]) % 2
+        ep[J] = ((T.astype(np.int64) @ sJ) % 2)[:len(J)]
+    e_hat[perm] = ep
+    return e_hat
