@@ -1,0 +1,140 @@
+/*
+ * qldpc_decoder.h — C ABI of the MI355X (gfx950) batched BP / Min-Sum decoder.
+ *
+ * This is the drop-in boundary for qLDPCsim's Monte-Carlo hot path
+ * (albertogp71/qLDPCsim @ 2025-12-26). The reference has no FFI: its boundary
+ * is the Python call dispatched per shot by simulate_p
+ * (qLDPCsim/simulator.py:270-284) into
+ *     MS_decoder(H, syndrome, p, max_iter=99, layers=None, beta=0.75,
+ *                OSDorder=-1, eps=1e-9) -> (e_hat int8[n], n_iter)   decoders.py:110-182
+ *     BP_decoder(H, syndrome, p, max_iter=99, layers=None, OSDorder=-1,
+ *                eps=1e-9) -> (e_hat int64[n], n_iter)               decoders.py:189-290
+ *     OSDdec(H, e_hat, syndrome, posteriorLLRs, order=0) -> e_hat      decoders.py:299-370
+ * Each entry point below names the reference interface it replaces. The
+ * Python package `qldpcsim_amd` binds these with ctypes and
+ * re-exposes the reference signatures unchanged.
+ *
+ * Conventions
+ *  - Plain C types only. Every function returns QLDPC_OK (0) or a negative
+ *    QLDPC_E* code; qldpc_last_error() gives a message (thread-local).
+ *  - "d_" pointers are device (HBM) pointers; "h_" pointers are host memory.
+ *  - `stream` is a hipStream_t passed as void* (NULL = the null stream).
+ *    Device entry points are asynchronous on that stream and do no
+ *    allocation, copy or synchronisation (hipGraph-capturable).
+ *  - Results are bit-exact with the reference for MS (hard decisions,
+ *    iteration counts, float64 posteriors) and within
+ *    1e-5 relative on BP posteriors (device tanh/atanh; App. A.2).
+ */
+#ifndef QLDPC_DECODER_H
+#define QLDPC_DECODER_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QLDPC_OK 0
+#define QLDPC_EINVAL -1   /* bad argument / shape / option   (reference: ValueError)  */
+#define QLDPC_ERANGE -2   /* index out of range               (reference: IndexError)  */
+#define QLDPC_EUNSUP -3   /* graph outside the kernel's limits (degree, size, LDS)     */
+#define QLDPC_EHIP -4     /* a HIP runtime call failed          (raised as RuntimeError) */
+#define QLDPC_ENOMEM -5
+
+#define QLDPC_ALGO_MS 0   /* normalized min-sum, decoders.py:110-182 */
+#define QLDPC_ALGO_BP 1   /* sum-product (tanh rule), decoders.py:189-290 */
+
+/* per-shot flag bits written to d_flags */
+#define QLDPC_FLAG_CONVERGED 1 /* a syndrome check passed (decoders.py:175-176 / :283-285) */
+#define QLDPC_FLAG_MIN_ZERO 2  /* MS: a check saw min|v|==0 (not emulated) */
+#define QLDPC_FLAG_NONFINITE 4 /* BP: tanh(v/2)==0 or a non-finite message */
+
+typedef struct qldpc_code qldpc_code;         /* Tanner graph of one H, resident in HBM */
+typedef struct qldpc_schedule qldpc_schedule; /* layer partition bound to one code     */
+
+const char *qldpc_last_error(void);
+const char *qldpc_version(void);
+
+/* Number of visible HIP devices (0 if none; never fails). */
+int qldpc_device_count(void);
+
+/* Build the Tanner graph of H (row-major uint8 m x n, entries taken mod 2,
+ * as load_matrix's `(mat % 2)`, simulator.py:35) and upload it to the current
+ * device. Replaces the per-call `np.where(H)` edge construction of
+ * BP_decoder (decoders.py:224-229) and MS_decoder's dense H masks
+ * (decoders.py:148-169). */
+int qldpc_code_create(const uint8_t *h_H, int m, int n, qldpc_code **out);
+int qldpc_code_destroy(qldpc_code *code);
+int qldpc_code_shape(const qldpc_code *code, int *m, int *n, int *n_edges);
+
+/* Bind a layer partition to a code: layer l holds rows
+ * h_layer_rows[h_layer_ptr[l] .. h_layer_ptr[l+1]). Replaces MS_decoder's /
+ * BP_decoder's `layers` list (decoders.py:114, :193, consumed at :154 / :247).
+ * One layer holding every row = flooding. Rows out of range -> QLDPC_ERANGE
+ * (reference: IndexError at decoders.py:156 / :250). Duplicate rows inside a
+ * layer are dropped (the reference's Jacobi update makes them idempotent). */
+int qldpc_schedule_create(const qldpc_code *code, int n_layers, const int32_t *h_layer_ptr,
+                          const int32_t *h_layer_rows, qldpc_schedule **out);
+int qldpc_schedule_destroy(qldpc_schedule *sched);
+
+/* Batched decode, device pointers, asynchronous on `stream`.
+ * Replaces `batch` calls of MS_decoder / BP_decoder (without the OSD
+ * post-step, which the host applies to non-converged shots via
+ * qldpc_osd_decode) — the inner loop of simulate_p (simulator.py:244-304).
+ *   d_syn   uint8 [batch][m]   syndrome bits (0/1)
+ *   p       prior error probability as passed to MS_decoder (simulate uses p/3)
+ *   beta    MS normalisation (0.75 default; ignored by BP)
+ *   eps     decoders.py's eps (1e-9)
+ *   d_ehat  uint8 [batch][n]   hard decisions, original column order
+ *   d_iters int32 [batch]      iterations as returned by the reference
+ *   d_post  double[batch][n]   final posterior LLRs (nullable)
+ *   d_flags int32 [batch]      QLDPC_FLAG_* (nullable) */
+int qldpc_decode_device(const qldpc_code *code, const qldpc_schedule *sched, int algo,
+                        const uint8_t *d_syn, int64_t batch, double p, int max_iter, double beta,
+                        double eps, uint8_t *d_ehat, int32_t *d_iters, double *d_post,
+                        int32_t *d_flags, void *stream);
+
+/* Same with host buffers: stages through device memory, synchronous.
+ * This is what the single-shot drop-in shims (MS_decoder / BP_decoder) use. */
+int qldpc_decode_host(const qldpc_code *code, const qldpc_schedule *sched, int algo,
+                      const uint8_t *h_syn, int64_t batch, double p, int max_iter, double beta,
+                      double eps, uint8_t *h_ehat, int32_t *h_iters, double *h_post,
+                      int32_t *h_flags);
+
+/* OSD post-decoder, host. Replaces OSDdec (decoders.py:299-370) including its
+ * aliasing semantics: order 0 -> solve;
+ * order 1 -> flip the first information-set position, then solve;
+ * order >= 2 -> identical to order 0. `h_ehat` (uint8[n]) is updated in place
+ * like the reference's `e_hat[perm] = ...` (decoders.py:368).
+ *   h_perm   int32[n]: np.argsort(reliability) as decoders.py:320-325 computes
+ *            it. The caller computes it with NumPy so that NumPy's own exp and
+ *            argsort decide near-ties exactly as in the reference.
+ *   h_J / h_J_size (nullable): the complementary information set (positions
+ *            in perm order, decoders.py:329-342), h_J sized n.
+ *   first_info_index: position the order-1 flip applies to (infoSet[0]);
+ *            -1 = emulate CPython's `list(set(range(n)) - set(J))[0]`.
+ * Errors: QLDPC_ERANGE where the reference raises IndexError (the greedy basis
+ * loop runs past column n-1). */
+int qldpc_osd_decode(const qldpc_code *code, const uint8_t *h_syn, const int32_t *h_perm, int order,
+                     uint8_t *h_ehat, int32_t *h_J, int32_t *h_J_size, int first_info_index);
+
+/* Batched OSD over `count` shots (syn uint8[count][m], perm int32[count][n],
+ * ehat uint8[count][n] in/out), `nthreads` host threads (<=0: hardware). */
+int qldpc_osd_decode_batch(const qldpc_code *code, int64_t count, const uint8_t *h_syn,
+                           const int32_t *h_perm, int order, uint8_t *h_ehat, int nthreads);
+
+/* First element of CPython's `set(range(n)) - set(J)` iteration order
+ * (the reference's infoSet[0], decoders.py:344); -1 if empty. */
+int qldpc_cpython_setdiff_first(int n, const int32_t *J, int nJ);
+
+/* Kernel timing (HIP events around each decode kernel launch, on the launch
+ * stream). Enabled by qldpc_timing_enable(1); qldpc_timing_read returns the
+ * summed kernel milliseconds and launch count since the last reset. */
+int qldpc_timing_enable(int on);
+int qldpc_timing_reset(void);
+int qldpc_timing_read(double *total_ms, int64_t *launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QLDPC_DECODER_H */

@@ -1,0 +1,176 @@
+"""ctypes binding of the C ABI in include/qldpc_decoder.h (libqldpc_hip.so).
+
+The product path has no CPU fallback: if the HIP library is missing this
+module raises on import, and every decode entry point fails loudly when no
+HIP device is visible.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("QLDPC_LIB", os.path.join(_HERE, "_build", "libqldpc_hip.so"))
+
+QLDPC_OK, QLDPC_EINVAL, QLDPC_ERANGE, QLDPC_EUNSUP, QLDPC_EHIP, QLDPC_ENOMEM = 0, -1, -2, -3, -4, -5
+ALGO = {"MS": 0, "BP": 1}
+FLAG_CONVERGED, FLAG_MIN_ZERO, FLAG_NONFINITE = 1, 2, 4
+
+# every symbol include/qldpc_decoder.h declares
+EXPORTS = (
+    "qldpc_last_error", "qldpc_version", "qldpc_device_count",
+    "qldpc_code_create", "qldpc_code_destroy", "qldpc_code_shape",
+    "qldpc_schedule_create", "qldpc_schedule_destroy",
+    "qldpc_decode_device", "qldpc_decode_host",
+    "qldpc_osd_decode", "qldpc_osd_decode_batch", "qldpc_cpython_setdiff_first",
+    "qldpc_timing_enable", "qldpc_timing_reset", "qldpc_timing_read",
+)
+
+
+class HIPLibraryMissing(ImportError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise HIPLibraryMissing(
+            f"{LIB_PATH} not found: build the HIP extension first "
+            "(`python -c 'import __graft_entry__ as g; g.build()'` or "
+            "`make -C qldpcsim_amd/csrc`). There is no CPU fallback.")
+    L = ctypes.CDLL(LIB_PATH)
+    P, I, D, I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_int64
+    PP = ctypes.POINTER(ctypes.c_void_p)
+    sig = {
+        "qldpc_last_error": ([], ctypes.c_char_p),
+        "qldpc_version": ([], ctypes.c_char_p),
+        "qldpc_device_count": ([], I),
+        "qldpc_code_create": ([P, I, I, PP], I),
+        "qldpc_code_destroy": ([P], I),
+        "qldpc_code_shape": ([P, P, P, P], I),
+        "qldpc_schedule_create": ([P, I, P, P, PP], I),
+        "qldpc_schedule_destroy": ([P], I),
+        "qldpc_decode_device": ([P, P, I, P, I64, D, I, D, D, P, P, P, P, P], I),
+        "qldpc_decode_host": ([P, P, I, P, I64, D, I, D, D, P, P, P, P], I),
+        "qldpc_osd_decode": ([P, P, P, I, P, P, P, I], I),
+        "qldpc_osd_decode_batch": ([P, I64, P, P, I, P, I], I),
+        "qldpc_cpython_setdiff_first": ([I, P, I], I),
+        "qldpc_timing_enable": ([I], I),
+        "qldpc_timing_reset": ([], I),
+        "qldpc_timing_read": ([P, P], I),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    return L
+
+
+lib = _load()
+
+
+def ptr(a):
+    """Raw address of a NumPy array (or None)."""
+    if a is None:
+        return None
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def check(rc):
+    if rc == QLDPC_OK:
+        return
+    msg = lib.qldpc_last_error().decode(errors="replace")
+    if rc == QLDPC_EINVAL:
+        raise ValueError(msg)
+    if rc == QLDPC_ERANGE:
+        raise IndexError(msg)
+    if rc == QLDPC_EUNSUP:
+        raise NotImplementedError(msg)
+    raise RuntimeError(f"qldpc error {rc}: {msg}")
+
+
+def device_count():
+    return int(lib.qldpc_device_count())
+
+
+class Schedule:
+    """A layer partition bound to a Code (qldpc_schedule)."""
+
+    def __init__(self, code, layer_ptr, layer_rows):
+        self.code = code
+        self.layer_ptr = np.ascontiguousarray(layer_ptr, dtype=np.int32)
+        self.layer_rows = np.ascontiguousarray(layer_rows, dtype=np.int32)
+        h = ctypes.c_void_p()
+        check(lib.qldpc_schedule_create(code.handle, len(self.layer_ptr) - 1, ptr(self.layer_ptr),
+                                        ptr(self.layer_rows), ctypes.byref(h)))
+        self.handle = h
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and lib is not None:
+            lib.qldpc_schedule_destroy(h)
+            self.handle = None
+
+
+class Code:
+    """Tanner graph of one parity-check matrix, resident on the current device."""
+
+    def __init__(self, H):
+        H = np.asarray(H)
+        if H.ndim != 2:
+            raise ValueError("H must be a 2-D matrix")
+        self.H = (H % 2).astype(np.uint8)
+        self.m, self.n = self.H.shape
+        h = ctypes.c_void_p()
+        Hc = np.ascontiguousarray(self.H)
+        check(lib.qldpc_code_create(ptr(Hc), self.m, self.n, ctypes.byref(h)))
+        self.handle = h
+        self._sched = {}
+        self._lock = threading.Lock()
+
+    def schedule(self, layer_ptr, layer_rows):
+        key = (np.asarray(layer_ptr, np.int32).tobytes(), np.asarray(layer_rows, np.int32).tobytes())
+        with self._lock:
+            s = self._sched.get(key)
+            if s is None:
+                s = Schedule(self, layer_ptr, layer_rows)
+                self._sched[key] = s
+            return s
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and lib is not None:
+            self._sched = {}
+            lib.qldpc_code_destroy(h)
+            self.handle = None
+
+
+_code_cache = {}
+_code_lock = threading.Lock()
+
+
+def code_for(H, device_index=None):
+    """Cached Code for a matrix (keyed by its bytes and the current device)."""
+    H = np.ascontiguousarray((np.asarray(H) % 2).astype(np.uint8))
+    key = (H.shape, H.tobytes(), device_index)
+    with _code_lock:
+        c = _code_cache.get(key)
+        if c is None:
+            c = Code(H)
+            _code_cache[key] = c
+        return c
+
+
+def timing_enable(on=True):
+    check(lib.qldpc_timing_enable(1 if on else 0))
+
+
+def timing_reset():
+    check(lib.qldpc_timing_reset())
+
+
+def timing_read():
+    ms = ctypes.c_double()
+    n = ctypes.c_int64()
+    check(lib.qldpc_timing_read(ctypes.byref(ms), ctypes.byref(n)))
+    return ms.value, n.value

@@ -1,0 +1,780 @@
+// capi.cpp — C ABI (include/qldpc_decoder.h): Tanner-graph preparation,
+// schedules, kernel launch configuration, host staging and timing.
+//
+// Replaces the per-call setup the reference repeats for every shot:
+//   BP_decoder's edge lists   np.where(H) + per-check/per-var lists  decoders.py:224-229
+//   MS_decoder's dense masks  H == 1 over m x n                       decoders.py:148-169
+// Here the graph is built once per H, bit-exactly ordered (CSR edges in
+// np.where(H) order; CSC lists in ascending check order), relabeled so that
+// variables of equal degree share wavefront passes, and uploaded once.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <thread>
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/qldpc_decoder.h"
+#include "decoder_kernels.h"
+
+using qldpc::DecodeArgs;
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess)                                                               \
+      return fail(QLDPC_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e),    \
+                  __FILE__, __LINE__);                                                  \
+  } while (0)
+
+extern "C" const char* qldpc_last_error(void) { return g_err.c_str(); }
+extern "C" const char* qldpc_version(void) { return "qldpcsim_amd 0.1.0 (gfx950)"; }
+
+extern "C" int qldpc_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+// ---------------------------------------------------------------------------
+// code (Tanner graph)
+// ---------------------------------------------------------------------------
+struct qldpc_code {
+  int m = 0, n = 0, E = 0, device = 0;
+  int uniform_deg = 0;  // row degree if every row has it, else 0
+  int max_row_deg = 0, max_col_deg = 0;
+  int rank = 0;         // GF(2) rank of H (gf2math.rank), for OSD
+  std::vector<int32_t> row_ptr, col_idx;     // CSR, np.where(H) order
+  std::vector<int32_t> vperm, vinv;          // relabeled -> original, original -> relabeled
+  std::vector<int32_t> csc_ptr, csc_edge;    // relabeled-variable CSC: CSR edge ids, ascending check
+  std::vector<int32_t> edge_pos;             // CSR edge -> CSC position
+  int mw = 0;                                // 64-bit words per column bit-vector
+  std::vector<uint64_t> col_bits;            // [n][mw] column j of H (OSD)
+  uint16_t* d_vinv = nullptr;
+  // host staging workspace for qldpc_decode_host
+  std::mutex ws_mu;
+  int64_t ws_cap = 0;
+  uint8_t *ws_syn = nullptr, *ws_ehat = nullptr;
+  int32_t *ws_iters = nullptr, *ws_flags = nullptr;
+  double* ws_post = nullptr;
+};
+
+static int gf2_rank_cols(const std::vector<uint64_t>& cols, int n, int mw);
+
+extern "C" int qldpc_code_create(const uint8_t* h_H, int m, int n, qldpc_code** out) {
+  if (!out) return fail(QLDPC_EINVAL, "out is null");
+  *out = nullptr;
+  if (m < 0 || n < 0 || (m * (int64_t)n > 0 && !h_H)) return fail(QLDPC_EINVAL, "bad shape %d x %d", m, n);
+  if (m > 65535 || n > 65535) return fail(QLDPC_EUNSUP, "matrix %d x %d exceeds 65535 rows/columns", m, n);
+  auto* c = new qldpc_code();
+  c->m = m;
+  c->n = n;
+  // No visible device (e.g. the CPU build container): the graph is still built
+  // so host-side services (OSD) work; decode entry points then fail loudly.
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0 || hipGetDevice(&c->device) != hipSuccess)
+    c->device = -1;
+  c->row_ptr.assign(m + 1, 0);
+  for (int r = 0; r < m; ++r) {
+    for (int j = 0; j < n; ++j)
+      if (h_H[(size_t)r * n + j] & 1) c->col_idx.push_back(j);  // (mat % 2) (simulator.py:35)
+    c->row_ptr[r + 1] = (int32_t)c->col_idx.size();
+  }
+  c->E = (int)c->col_idx.size();
+  if (c->E > 65535) {
+    delete c;
+    return fail(QLDPC_EUNSUP, "%d edges exceed the 65535-edge limit of the 16-bit graph tables", (int)c->col_idx.size());
+  }
+  std::vector<int> cdeg(n, 0);
+  for (int e = 0; e < c->E; ++e) cdeg[c->col_idx[e]]++;
+  for (int r = 0; r < m; ++r) c->max_row_deg = std::max(c->max_row_deg, c->row_ptr[r + 1] - c->row_ptr[r]);
+  for (int j = 0; j < n; ++j) c->max_col_deg = std::max(c->max_col_deg, cdeg[j]);
+  c->uniform_deg = m > 0 ? c->row_ptr[1] : 0;
+  for (int r = 0; r < m; ++r)
+    if (c->row_ptr[r + 1] - c->row_ptr[r] != c->uniform_deg) c->uniform_deg = 0;
+  // Relabel variables by degree (stable) so a wavefront pass over 64
+  // consecutive relabeled variables has (nearly) one loop trip count.
+  c->vperm.resize(n);
+  for (int j = 0; j < n; ++j) c->vperm[j] = j;
+  std::stable_sort(c->vperm.begin(), c->vperm.end(), [&](int a, int b) { return cdeg[a] < cdeg[b]; });
+  c->vinv.resize(n);
+  for (int r = 0; r < n; ++r) c->vinv[c->vperm[r]] = r;
+  // CSC over relabeled variables; CSR traversal in ascending row keeps each
+  // column's list in ascending check order (np.sum axis=0 order).
+  c->csc_ptr.assign(n + 1, 0);
+  for (int r = 0; r < n; ++r) c->csc_ptr[r + 1] = c->csc_ptr[r] + cdeg[c->vperm[r]];
+  c->csc_edge.assign(c->E, 0);
+  c->edge_pos.assign(c->E, 0);
+  std::vector<int32_t> fill(c->csc_ptr.begin(), c->csc_ptr.end() - 1);
+  for (int r = 0; r < m; ++r)
+    for (int e = c->row_ptr[r]; e < c->row_ptr[r + 1]; ++e) {
+      const int pos = fill[c->vinv[c->col_idx[e]]]++;
+      c->csc_edge[pos] = e;
+      c->edge_pos[e] = pos;
+    }
+  // column bit-vectors for OSD
+  c->mw = (m + 63) / 64;
+  c->col_bits.assign((size_t)n * std::max(c->mw, 1), 0);
+  for (int r = 0; r < m; ++r)
+    for (int e = c->row_ptr[r]; e < c->row_ptr[r + 1]; ++e)
+      c->col_bits[(size_t)c->col_idx[e] * c->mw + (r >> 6)] |= 1ull << (r & 63);
+  c->rank = gf2_rank_cols(c->col_bits, n, c->mw);
+  if (n > 0 && c->device >= 0) {
+    std::vector<uint16_t> v16(c->vinv.begin(), c->vinv.end());
+    hipError_t e1 = hipMalloc(&c->d_vinv, sizeof(uint16_t) * n);
+    if (e1 == hipSuccess) e1 = hipMemcpy(c->d_vinv, v16.data(), sizeof(uint16_t) * n, hipMemcpyHostToDevice);
+    if (e1 != hipSuccess) {
+      delete c;
+      return fail(QLDPC_EHIP, "uploading the graph failed: %s", hipGetErrorString(e1));
+    }
+  }
+  *out = c;
+  return QLDPC_OK;
+}
+
+static void ws_free(qldpc_code* c) {
+  (void)hipFree(c->ws_syn);
+  (void)hipFree(c->ws_ehat);
+  (void)hipFree(c->ws_iters);
+  (void)hipFree(c->ws_flags);
+  (void)hipFree(c->ws_post);
+  c->ws_syn = c->ws_ehat = nullptr;
+  c->ws_iters = c->ws_flags = nullptr;
+  c->ws_post = nullptr;
+  c->ws_cap = 0;
+}
+
+extern "C" int qldpc_code_destroy(qldpc_code* code) {
+  if (!code) return QLDPC_OK;
+  (void)hipFree(code->d_vinv);
+  ws_free(code);
+  delete code;
+  return QLDPC_OK;
+}
+
+extern "C" int qldpc_code_shape(const qldpc_code* code, int* m, int* n, int* n_edges) {
+  if (!code) return fail(QLDPC_EINVAL, "code is null");
+  if (m) *m = code->m;
+  if (n) *n = code->n;
+  if (n_edges) *n_edges = code->E;
+  return QLDPC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// schedule (layers) + LDS image
+// ---------------------------------------------------------------------------
+struct LaunchCfg {
+  const void* kernel = nullptr;
+  int waves = 0, blocks_per_cu = 0, lds = 0, wave_bytes = 0;
+  bool ok = false;
+};
+
+struct qldpc_schedule {
+  const qldpc_code* code = nullptr;
+  bool layered = false;
+  int n_layers = 0;
+  std::vector<uint8_t> blob;  // LDS image of the graph tables
+  int off_cn_tab = 0, off_row_ptr = 0, off_vn_ptr = 0, off_vn_chk = 0;
+  int off_lay_ptr = 0, off_lay_rows = 0, off_adj_ptr = 0, off_adj_vars = 0;
+  unsigned char* d_blob = nullptr;
+  LaunchCfg cfg[2];           // per algo
+  std::mutex mu;
+};
+
+static int align16(int x) { return (x + 15) & ~15; }
+
+template <typename T>
+static int put(std::vector<uint8_t>& blob, const std::vector<T>& v) {
+  const int off = align16((int)blob.size());
+  blob.resize(off + sizeof(T) * v.size());
+  if (!v.empty()) memcpy(blob.data() + off, v.data(), sizeof(T) * v.size());
+  return off;
+}
+
+extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const int32_t* h_layer_ptr,
+                                     const int32_t* h_layer_rows, qldpc_schedule** out) {
+  if (!out) return fail(QLDPC_EINVAL, "out is null");
+  *out = nullptr;
+  if (!code) return fail(QLDPC_EINVAL, "code is null");
+  if (n_layers < 0 || (n_layers > 0 && !h_layer_ptr)) return fail(QLDPC_EINVAL, "bad layer list");
+  const int m = code->m, n = code->n;
+  std::vector<std::vector<int>> layers(n_layers);
+  for (int l = 0; l < n_layers; ++l) {
+    const int a = h_layer_ptr[l], b = h_layer_ptr[l + 1];
+    if (a < 0 || b < a) return fail(QLDPC_EINVAL, "layer_ptr is not non-decreasing at layer %d", l);
+    std::vector<char> seen(m, 0);
+    for (int q = a; q < b; ++q) {
+      const int r = h_layer_rows[q];
+      if (r < 0 || r >= m)
+        return fail(QLDPC_ERANGE, "index %d is out of bounds for axis 0 with size %d", r, m);
+      if (!seen[r]) {  // duplicates inside a layer: same Jacobi inputs, same outputs
+        seen[r] = 1;
+        layers[l].push_back(r);
+      }
+    }
+  }
+  auto* s = new qldpc_schedule();
+  s->code = code;
+  s->n_layers = n_layers;
+  // One layer holding every row exactly once == flooding (decoders.py:122).
+  s->layered = !(n_layers == 1 && (int)layers[0].size() == m);
+
+  std::vector<uint32_t> cn_tab(code->E);
+  for (int e = 0; e < code->E; ++e)
+    cn_tab[e] = ((uint32_t)code->vinv[code->col_idx[e]] << 16) | (uint32_t)code->edge_pos[e];
+  std::vector<uint16_t> row_ptr(code->row_ptr.begin(), code->row_ptr.end());
+  std::vector<uint16_t> vn_ptr(code->csc_ptr.begin(), code->csc_ptr.end());
+  s->off_cn_tab = put(s->blob, cn_tab);
+  s->off_row_ptr = put(s->blob, row_ptr);
+  s->off_vn_ptr = put(s->blob, vn_ptr);
+  if (s->layered) {
+    std::vector<uint16_t> vn_chk(code->E), lay_ptr(n_layers + 1, 0), lay_rows, adj_ptr(n_layers + 1, 0), adj_vars;
+    for (int p = 0; p < code->E; ++p) {
+      // CSR edge -> its check (row)
+      const int e = code->csc_edge[p];
+      const int r = (int)(std::upper_bound(code->row_ptr.begin(), code->row_ptr.end(), e) - code->row_ptr.begin()) - 1;
+      vn_chk[p] = (uint16_t)r;
+    }
+    std::vector<int> mark(n, -1);
+    for (int l = 0; l < n_layers; ++l) {
+      std::vector<int> adj;
+      for (int r : layers[l]) {
+        lay_rows.push_back((uint16_t)r);
+        for (int e = code->row_ptr[r]; e < code->row_ptr[r + 1]; ++e) {
+          const int v = code->vinv[code->col_idx[e]];
+          if (mark[v] != l) {
+            mark[v] = l;
+            adj.push_back(v);
+          }
+        }
+      }
+      std::sort(adj.begin(), adj.end());
+      for (int v : adj) adj_vars.push_back((uint16_t)v);
+      if (lay_rows.size() > 65535 || adj_vars.size() > 65535) {
+        delete s;
+        return fail(QLDPC_EUNSUP, "schedule too large for 16-bit layer tables");
+      }
+      lay_ptr[l + 1] = (uint16_t)lay_rows.size();
+      adj_ptr[l + 1] = (uint16_t)adj_vars.size();
+    }
+    s->off_vn_chk = put(s->blob, vn_chk);
+    s->off_lay_ptr = put(s->blob, lay_ptr);
+    s->off_lay_rows = put(s->blob, lay_rows);
+    s->off_adj_ptr = put(s->blob, adj_ptr);
+    s->off_adj_vars = put(s->blob, adj_vars);
+  }
+  s->blob.resize(align16((int)s->blob.size() + 1));
+  if (code->device < 0) {  // no device: keep the host image only
+    *out = s;
+    return QLDPC_OK;
+  }
+  hipError_t e1 = hipMalloc(&s->d_blob, s->blob.size());
+  if (e1 == hipSuccess) e1 = hipMemcpy(s->d_blob, s->blob.data(), s->blob.size(), hipMemcpyHostToDevice);
+  if (e1 != hipSuccess) {
+    delete s;
+    return fail(QLDPC_EHIP, "uploading the schedule failed: %s", hipGetErrorString(e1));
+  }
+  *out = s;
+  return QLDPC_OK;
+}
+
+extern "C" int qldpc_schedule_destroy(qldpc_schedule* s) {
+  if (!s) return QLDPC_OK;
+  (void)hipFree(s->d_blob);
+  delete s;
+  return QLDPC_OK;
+}
+
+// per-wave state slice: post f64[n] | c2v (f32|f64)[E] | syn words | parity words
+static void wave_layout(const qldpc_code* c, bool layered, int algo, int* bytes, int* off_c2v,
+                        int* off_synw, int* off_parw) {
+  int off = align16(8 * c->n);
+  *off_c2v = off;
+  off = align16(off + (algo == QLDPC_ALGO_MS ? 4 : 8) * c->E);
+  const int words = 2 * ((c->m + 63) / 64);
+  *off_synw = off;
+  if (layered) off = align16(off + 4 * words);
+  *off_parw = off;
+  if (layered) off = align16(off + 4 * words);
+  *bytes = std::max(off, 16);
+}
+
+static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
+  std::lock_guard<std::mutex> lk(s->mu);
+  LaunchCfg& cfg = s->cfg[algo];
+  if (cfg.ok) {
+    *out = &cfg;
+    return QLDPC_OK;
+  }
+  const qldpc_code* c = s->code;
+  const int dc = (c->uniform_deg == 7 || c->uniform_deg == 8) ? c->uniform_deg : 0;
+  cfg.kernel = qldpc::select_kernel(algo, s->layered, dc);
+  int off_c2v, off_synw, off_parw;
+  wave_layout(c, s->layered, algo, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw);
+  int max_lds = 0, dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  HIP_TRY(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
+  HIP_TRY(qldpc::configure_kernel(cfg.kernel, max_lds));
+  const int blob = (int)s->blob.size();
+  int best_waves = 0;
+  for (int w = 16; w >= 1; --w) {
+    const int lds = blob + w * cfg.wave_bytes;
+    if (lds > max_lds) continue;
+    int nb = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cfg.kernel, 64 * w, (size_t)lds));
+    if (nb * w > best_waves) {
+      best_waves = nb * w;
+      cfg.waves = w;
+      cfg.blocks_per_cu = nb;
+      cfg.lds = lds;
+    }
+  }
+  if (best_waves == 0)
+    return fail(QLDPC_EUNSUP, "graph needs %d B of LDS per wave plus %d B of tables: exceeds %d B",
+                cfg.wave_bytes, blob, max_lds);
+  cfg.ok = true;
+  *out = &cfg;
+  return QLDPC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// timing
+// ---------------------------------------------------------------------------
+static std::mutex g_tmu;
+static bool g_timing = false;
+static std::vector<std::pair<hipEvent_t, hipEvent_t>> g_events;
+static double g_total_ms = 0.0;
+static int64_t g_launches = 0;
+
+extern "C" int qldpc_timing_enable(int on) {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  g_timing = on != 0;
+  return QLDPC_OK;
+}
+
+static int drain_events_locked() {
+  for (auto& ev : g_events) {
+    HIP_TRY(hipEventSynchronize(ev.second));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, ev.first, ev.second));
+    g_total_ms += ms;
+    g_launches++;
+    (void)hipEventDestroy(ev.first);
+    (void)hipEventDestroy(ev.second);
+  }
+  g_events.clear();
+  return QLDPC_OK;
+}
+
+extern "C" int qldpc_timing_reset(void) {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  int rc = drain_events_locked();
+  g_total_ms = 0.0;
+  g_launches = 0;
+  return rc;
+}
+
+extern "C" int qldpc_timing_read(double* total_ms, int64_t* launches) {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  int rc = drain_events_locked();
+  if (total_ms) *total_ms = g_total_ms;
+  if (launches) *launches = g_launches;
+  return rc;
+}
+
+// ---------------------------------------------------------------------------
+// decode
+// ---------------------------------------------------------------------------
+extern "C" int qldpc_decode_device(const qldpc_code* code, const qldpc_schedule* sched_c, int algo,
+                                   const uint8_t* d_syn, int64_t batch, double p, int max_iter,
+                                   double beta, double eps, uint8_t* d_ehat, int32_t* d_iters,
+                                   double* d_post, int32_t* d_flags, void* stream) {
+  auto* sched = const_cast<qldpc_schedule*>(sched_c);
+  if (!code || !sched) return fail(QLDPC_EINVAL, "code/schedule is null");
+  if (sched->code != code) return fail(QLDPC_EINVAL, "schedule was built for a different code");
+  if (algo != QLDPC_ALGO_MS && algo != QLDPC_ALGO_BP) return fail(QLDPC_EINVAL, "Unrecognized decoder type.");
+  if (batch < 0) return fail(QLDPC_EINVAL, "negative batch");
+  if (max_iter < 1) return fail(QLDPC_EINVAL, "max_iter must be >= 1 (the reference leaves e_hat unbound)");
+  if (batch == 0) return QLDPC_OK;
+  if (!d_syn || !d_ehat || !d_iters) return fail(QLDPC_EINVAL, "null device buffer");
+  if (algo == QLDPC_ALGO_MS && code->max_row_deg > 32)
+    return fail(QLDPC_EUNSUP, "min-sum kernel supports row degree <= 32 (got %d)", code->max_row_deg);
+  if (algo == QLDPC_ALGO_BP && code->max_col_deg > 128)
+    return fail(QLDPC_EUNSUP, "BP kernel supports column degree <= 128 (got %d)", code->max_col_deg);
+  if (code->device < 0 || !sched->d_blob) return fail(QLDPC_EHIP, "no HIP device was visible when the code/schedule was created");
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  if (dev != code->device) return fail(QLDPC_EINVAL, "code lives on device %d, current device is %d", code->device, dev);
+  LaunchCfg* cfg = nullptr;
+  int rc = launch_config(sched, algo, &cfg);
+  if (rc) return rc;
+
+  DecodeArgs a{};
+  a.blob = sched->d_blob;
+  a.blob_bytes = (int)sched->blob.size();
+  a.off_cn_tab = sched->off_cn_tab;
+  a.off_row_ptr = sched->off_row_ptr;
+  a.off_vn_ptr = sched->off_vn_ptr;
+  a.off_vn_chk = sched->off_vn_chk;
+  a.off_lay_ptr = sched->off_lay_ptr;
+  a.off_lay_rows = sched->off_lay_rows;
+  a.off_adj_ptr = sched->off_adj_ptr;
+  a.off_adj_vars = sched->off_adj_vars;
+  wave_layout(code, sched->layered, algo, &a.wave_bytes, &a.off_c2v, &a.off_synw, &a.off_parw);
+  a.m = code->m;
+  a.n = code->n;
+  a.E = code->E;
+  a.n_layers = sched->n_layers;
+  a.vinv = code->d_vinv;
+  a.syn = d_syn;
+  a.ehat = d_ehat;
+  a.iters = d_iters;
+  a.post = d_post;
+  a.flags = d_flags;
+  a.batch = batch;
+  // L_ch = np.log((1 - p) / max(p, eps))   (decoders.py:147, :232)
+  a.L = std::log((1.0 - p) / std::max(p, eps));
+  a.L32 = (float)a.L;
+  a.beta = beta;
+  a.eps = eps;
+  a.max_iter = max_iter;
+
+  int cus = 0;
+  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const int64_t need = (batch + cfg->waves - 1) / cfg->waves;
+  const int64_t resident = (int64_t)cfg->blocks_per_cu * cus;
+  const int grid = (int)std::max<int64_t>(1, std::min(need, resident));
+  hipStream_t st = (hipStream_t)stream;
+
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  bool timed;
+  {
+    std::lock_guard<std::mutex> lk(g_tmu);
+    timed = g_timing;
+  }
+  if (timed) {
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipEventRecord(e0, st));
+  }
+  HIP_TRY(qldpc::launch_decode(cfg->kernel, a, grid, 64 * cfg->waves, cfg->lds, st));
+  if (timed) {
+    HIP_TRY(hipEventRecord(e1, st));
+    std::lock_guard<std::mutex> lk(g_tmu);
+    g_events.emplace_back(e0, e1);
+  }
+  return QLDPC_OK;
+}
+
+extern "C" int qldpc_decode_host(const qldpc_code* code_c, const qldpc_schedule* sched, int algo,
+                                 const uint8_t* h_syn, int64_t batch, double p, int max_iter,
+                                 double beta, double eps, uint8_t* h_ehat, int32_t* h_iters,
+                                 double* h_post, int32_t* h_flags) {
+  auto* code = const_cast<qldpc_code*>(code_c);
+  if (!code) return fail(QLDPC_EINVAL, "code is null");
+  if (batch < 0) return fail(QLDPC_EINVAL, "negative batch");
+  if (batch == 0) return QLDPC_OK;
+  if (!h_syn || !h_ehat || !h_iters) return fail(QLDPC_EINVAL, "null host buffer");
+  std::lock_guard<std::mutex> lk(code->ws_mu);
+  const int m = code->m, n = code->n;
+  if (batch > code->ws_cap) {
+    ws_free(code);
+    const int64_t cap = std::max<int64_t>(batch, 64);
+    HIP_TRY(hipMalloc(&code->ws_syn, std::max<int64_t>(1, cap * m)));
+    HIP_TRY(hipMalloc(&code->ws_ehat, std::max<int64_t>(1, cap * n)));
+    HIP_TRY(hipMalloc(&code->ws_iters, sizeof(int32_t) * cap));
+    HIP_TRY(hipMalloc(&code->ws_flags, sizeof(int32_t) * cap));
+    HIP_TRY(hipMalloc(&code->ws_post, sizeof(double) * std::max<int64_t>(1, cap * n)));
+    code->ws_cap = cap;
+  }
+  if (batch * m) HIP_TRY(hipMemcpy(code->ws_syn, h_syn, batch * m, hipMemcpyHostToDevice));
+  int rc = qldpc_decode_device(code, sched, algo, code->ws_syn, batch, p, max_iter, beta, eps,
+                               code->ws_ehat, code->ws_iters, h_post ? code->ws_post : nullptr,
+                               code->ws_flags, nullptr);
+  if (rc) return rc;
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipDeviceSynchronize());
+  if (batch * n) HIP_TRY(hipMemcpy(h_ehat, code->ws_ehat, batch * n, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(h_iters, code->ws_iters, sizeof(int32_t) * batch, hipMemcpyDeviceToHost));
+  if (h_flags) HIP_TRY(hipMemcpy(h_flags, code->ws_flags, sizeof(int32_t) * batch, hipMemcpyDeviceToHost));
+  if (h_post && batch * n)
+    HIP_TRY(hipMemcpy(h_post, code->ws_post, sizeof(double) * batch * n, hipMemcpyDeviceToHost));
+  return QLDPC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// GF(2) rank of H by XOR-basis insertion of its columns (gf2math.rank,
+// gf2math.py:91-135 — rank is basis independent).
+// ---------------------------------------------------------------------------
+struct Gf2Basis {
+  int mw;
+  std::vector<uint64_t> vec;  // [m][mw], slot b holds a vector whose lowest set bit is b
+  std::vector<char> has;
+  Gf2Basis(int m, int mw_) : mw(mw_), vec((size_t)std::max(m, 1) * std::max(mw_, 1), 0), has(std::max(m, 1), 0) {}
+  // returns true if x (modified) was independent and got inserted
+  bool insert(uint64_t* x) {
+    for (int w = 0; w < mw; ++w) {
+      while (x[w]) {
+        const int b = w * 64 + __builtin_ctzll(x[w]);
+        if (!has[b]) {
+          memcpy(&vec[(size_t)b * mw], x, sizeof(uint64_t) * mw);
+          has[b] = 1;
+          return true;
+        }
+        const uint64_t* v = &vec[(size_t)b * mw];
+        for (int k = w; k < mw; ++k) x[k] ^= v[k];
+      }
+    }
+    return false;
+  }
+};
+
+static int gf2_rank_cols(const std::vector<uint64_t>& cols, int n, int mw) {
+  if (mw == 0) return 0;
+  Gf2Basis B(mw * 64, mw);
+  std::vector<uint64_t> x(mw);
+  int r = 0;
+  for (int j = 0; j < n; ++j) {
+    memcpy(x.data(), &cols[(size_t)j * mw], sizeof(uint64_t) * mw);
+    r += B.insert(x.data());
+  }
+  return r;
+}
+
+// Order of iteration of CPython's `set(range(n)) - set(J)` (the reference's
+// infoSet, decoders.py:344): returns its first element. Emulates
+// setobject.c (set_difference -> set_add_entry / set_table_resize /
+// set_insert_clean; LINEAR_PROBES 9, PERTURB_SHIFT 5) for small-int keys
+// (hash(i) == i). Verified against the interpreter in tests.
+static int cpython_setdiff_first(int n, const std::vector<char>& inJ, int nJ) {
+  if (nJ == n) return -1;
+  if ((n >> 2) > nJ) {
+    // set_copy_and_difference: a copy of set(range(n)) (ascending slots)
+    for (int i = 0; i < n; ++i)
+      if (!inJ[i]) return i;
+    return -1;
+  }
+  size_t mask = 7;
+  std::vector<int64_t> table(8, -1);
+  size_t fill = 0, used = 0;
+  auto insert_clean = [](std::vector<int64_t>& t, size_t msk, int64_t key) {
+    size_t perturb = (size_t)key, i = (size_t)key & msk;
+    while (true) {
+      if (t[i] < 0) { t[i] = key; return; }
+      if (i + 9 <= msk) {
+        for (int j = 0; j < 9; ++j) {
+          ++i;
+          if (t[i] < 0) { t[i] = key; return; }
+        }
+      }
+      perturb >>= 5;
+      i = (i * 5 + 1 + perturb) & msk;
+    }
+  };
+  for (int key = 0; key < n; ++key) {
+    if (inJ[key]) continue;
+    // set_add_entry (new key, no dummies)
+    size_t perturb = (size_t)key, i = (size_t)key & mask;
+    while (true) {
+      size_t probes = (i + 9 <= mask) ? 9 : 0;
+      size_t k = i;
+      bool placed = false;
+      while (true) {
+        if (table[k] < 0) {
+          table[k] = key;
+          placed = true;
+          break;
+        }
+        if (probes-- == 0) break;
+        ++k;
+      }
+      if (placed) break;
+      perturb >>= 5;
+      i = (i * 5 + 1 + perturb) & mask;
+    }
+    ++fill;
+    ++used;
+    if (fill * 5 >= mask * 3) {
+      const size_t minused = used > 50000 ? used * 2 : used * 4;
+      size_t newsize = 8;
+      while (newsize <= minused) newsize <<= 1;
+      std::vector<int64_t> nt(newsize, -1);
+      for (size_t s2 = 0; s2 <= mask; ++s2)
+        if (table[s2] >= 0) insert_clean(nt, newsize - 1, table[s2]);
+      table.swap(nt);
+      mask = newsize - 1;
+    }
+  }
+  for (size_t s2 = 0; s2 <= mask; ++s2)
+    if (table[s2] >= 0) return (int)table[s2];
+  return -1;
+}
+
+extern "C" int qldpc_cpython_setdiff_first(int n, const int32_t* J, int nJ) {
+  std::vector<char> inJ(std::max(n, 1), 0);
+  int cnt = 0;
+  for (int k = 0; k < nJ; ++k)
+    if (J[k] >= 0 && J[k] < n && !inJ[J[k]]) inJ[J[k]] = 1, ++cnt;
+  return cpython_setdiff_first(n, inJ, cnt);
+}
+
+// ---------------------------------------------------------------------------
+// OSD (decoders.py:299-370), given the caller's reliability order `perm`
+// (np.argsort of decoders.py:320-325 — NumPy's own exp/argsort decide ties).
+// ---------------------------------------------------------------------------
+static int osd_one(const qldpc_code* c, const uint8_t* syn, const int32_t* perm, int order, uint8_t* ehat,
+                   int32_t* J_out, int32_t* J_size, int first_info_index) {
+  const int m = c->m, n = c->n, mw = c->mw;
+  if (n == 0) return QLDPC_OK;
+  // (1) least reliable basis J (decoders.py:329-342): index 0 unconditionally,
+  //     then every column (in perm order) that raises the rank, until rank(H).
+  Gf2Basis B(std::max(mw * 64, 1), mw);
+  std::vector<uint64_t> x(std::max(mw, 1));
+  std::vector<int> J;
+  std::vector<char> inJ(n, 0);
+  auto col = [&](int i) { return &c->col_bits[(size_t)perm[i] * mw]; };
+  if (mw) memcpy(x.data(), col(0), sizeof(uint64_t) * mw);
+  int rank = mw ? (int)B.insert(x.data()) : 0;
+  J.push_back(0);
+  inJ[0] = 1;
+  if (rank >= c->rank)
+    return fail(QLDPC_ERANGE, "index %d is out of bounds for axis 1 with size %d", n, n);  // reference IndexError
+  int next = 1;
+  while (true) {
+    if (next >= n) return fail(QLDPC_ERANGE, "index %d is out of bounds for axis 1 with size %d", n, n);
+    memcpy(x.data(), col(next), sizeof(uint64_t) * mw);
+    if (B.insert(x.data())) {
+      J.push_back(next);
+      inJ[next] = 1;
+      if (++rank >= c->rank) break;
+    }
+    ++next;
+  }
+  const int nJ = (int)J.size();
+  if (J_out)
+    for (int k = 0; k < nJ; ++k) J_out[k] = J[k];
+  if (J_size) *J_size = nJ;
+  // (2) e_hat_perm = e_hat[perm]; order-k loop with aliasing:
+  //     the cumulative flip is I[0] for order 1 and nothing otherwise.
+  std::vector<uint8_t> ep(n);
+  for (int i = 0; i < n; ++i) ep[i] = ehat[perm[i]] & 1;
+  if (order == 1 && nJ < n) {
+    int i0 = first_info_index >= 0 ? first_info_index : cpython_setdiff_first(n, inJ, nJ);
+    if (i0 < 0 || i0 >= n || inJ[i0]) return fail(QLDPC_EINVAL, "bad first_info_index %d", i0);
+    ep[i0] ^= 1;
+  }
+  // (3) sJ = (syndrome + Hp[:, I] @ e_I) % 2
+  std::vector<uint64_t> sJ(std::max(mw, 1), 0);
+  for (int r = 0; r < m; ++r)
+    if (syn[r] & 1) sJ[r >> 6] |= 1ull << (r & 63);
+  for (int i = 0; i < n; ++i)
+    if (!inJ[i] && ep[i]) {
+      const uint64_t* cb = col(i);
+      for (int w = 0; w < mw; ++w) sJ[w] ^= cb[w];
+    }
+  // (4) (T @ sJ) % 2 with T from REF(Hp[:, J], reduced=True) (gf2math.py:139-187):
+  //     the same row operations applied to sJ as an augmented column.
+  const int rw = (nJ + 63) / 64;
+  std::vector<uint64_t> rows((size_t)m * rw, 0);
+  for (int k = 0; k < nJ; ++k) {
+    const uint64_t* cb = col(J[k]);
+    for (int w = 0; w < mw; ++w) {
+      uint64_t bits = cb[w];
+      while (bits) {
+        const int r = w * 64 + __builtin_ctzll(bits);
+        bits &= bits - 1;
+        rows[(size_t)r * rw + (k >> 6)] |= 1ull << (k & 63);
+      }
+    }
+  }
+  std::vector<uint8_t> s(m);
+  for (int r = 0; r < m; ++r) s[r] = (sJ[r >> 6] >> (r & 63)) & 1;
+  auto bit = [&](int r, int k) { return (rows[(size_t)r * rw + (k >> 6)] >> (k & 63)) & 1; };
+  auto xor_row = [&](int dst, int src) {
+    for (int w = 0; w < rw; ++w) rows[(size_t)dst * rw + w] ^= rows[(size_t)src * rw + w];
+    s[dst] ^= s[src];
+  };
+  int xr = 0;
+  for (int k = 0; k < nJ && m > 0; ++k) {
+    int r = xr;
+    while (r < m && !bit(r, k)) ++r;
+    if (r == m) continue;
+    if (r != xr) {
+      for (int w = 0; w < rw; ++w) std::swap(rows[(size_t)xr * rw + w], rows[(size_t)r * rw + w]);
+      std::swap(s[xr], s[r]);
+    }
+    for (int t = r + 1; t < m; ++t)
+      if (bit(t, k)) xor_row(t, xr);
+    for (int t = 0; t < xr; ++t)
+      if (bit(t, k)) xor_row(t, xr);
+    if (++xr >= m) break;
+  }
+  for (int k = 0; k < nJ; ++k) ep[J[k]] = k < m ? s[k] : 0;
+  for (int i = 0; i < n; ++i) ehat[perm[i]] = ep[i];  // e_hat[perm] = ... (:368)
+  return QLDPC_OK;
+}
+
+extern "C" int qldpc_osd_decode(const qldpc_code* code, const uint8_t* h_syn, const int32_t* h_perm, int order,
+                                uint8_t* h_ehat, int32_t* h_J, int32_t* h_J_size, int first_info_index) {
+  if (!code || !h_perm || !h_ehat || (!h_syn && code->m)) return fail(QLDPC_EINVAL, "null argument");
+  std::vector<char> seen(code->n, 0);
+  for (int i = 0; i < code->n; ++i) {
+    if (h_perm[i] < 0 || h_perm[i] >= code->n || seen[h_perm[i]]) return fail(QLDPC_EINVAL, "perm is not a permutation");
+    seen[h_perm[i]] = 1;
+  }
+  return osd_one(code, h_syn, h_perm, order, h_ehat, h_J, h_J_size, first_info_index);
+}
+
+extern "C" int qldpc_osd_decode_batch(const qldpc_code* code, int64_t count, const uint8_t* h_syn,
+                                      const int32_t* h_perm, int order, uint8_t* h_ehat, int nthreads) {
+  if (!code) return fail(QLDPC_EINVAL, "code is null");
+  if (count <= 0) return QLDPC_OK;
+  if (nthreads <= 0) nthreads = (int)std::max(1u, std::thread::hardware_concurrency());
+  nthreads = (int)std::min<int64_t>(nthreads, count);
+  const int m = code->m, n = code->n;
+  std::atomic<int64_t> next{0};
+  std::atomic<int> rc{QLDPC_OK};
+  std::string err;
+  std::mutex emu;
+  auto worker = [&]() {
+    while (true) {
+      const int64_t b = next.fetch_add(1);
+      if (b >= count || rc.load() != QLDPC_OK) return;
+      const int r = qldpc_osd_decode(code, h_syn + b * m, h_perm + b * n, order, h_ehat + b * n,
+                                     nullptr, nullptr, -1);
+      if (r != QLDPC_OK) {
+        std::lock_guard<std::mutex> lk(emu);
+        if (rc.load() == QLDPC_OK) err = g_err;
+        rc = r;
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nthreads; ++t) th.emplace_back(worker);
+  worker();
+  for (auto& t : th) t.join();
+  if (rc.load() != QLDPC_OK) g_err = err;
+  return rc.load();
+}

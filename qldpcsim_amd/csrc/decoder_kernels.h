@@ -1,0 +1,39 @@
+// decoder_kernels.h — shared between the HIP kernels and the C-ABI host code.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace qldpc {
+
+enum { ALGO_MS = 0, ALGO_BP = 1 };
+enum { FLAG_CONVERGED = 1, FLAG_MIN_ZERO = 2, FLAG_NONFINITE = 4 };
+
+// Kernel arguments (by value). Offsets are byte offsets inside the LDS image:
+// [blob (graph tables, staged from `blob`)][wave 0 state][wave 1 state]...
+struct DecodeArgs {
+  const unsigned char* blob;  // device copy of the LDS table image
+  int blob_bytes;             // multiple of 16
+  int off_cn_tab, off_row_ptr, off_vn_ptr, off_vn_chk;
+  int off_lay_ptr, off_lay_rows, off_adj_ptr, off_adj_vars;
+  int wave_bytes;             // per-wave state slice (multiple of 16)
+  int off_c2v, off_synw, off_parw;  // inside a wave slice (post f64[n] at 0)
+  int m, n, E, n_layers;
+  const uint16_t* vinv;       // [n] original column -> relabeled variable (global)
+  const uint8_t* syn;         // [batch][m]
+  uint8_t* ehat;              // [batch][n]
+  int32_t* iters;             // [batch]
+  double* post;               // [batch][n] or null
+  int32_t* flags;             // [batch] or null
+  long long batch;
+  double L;                   // log((1-p)/max(p,eps))
+  float L32;                  // float32(L)
+  double beta, eps;
+  int max_iter;
+};
+
+const void* select_kernel(int algo, bool layered, int dc);
+hipError_t launch_decode(const void* kernel, const DecodeArgs& args, int grid, int block,
+                         int lds_bytes, hipStream_t stream);
+hipError_t configure_kernel(const void* kernel, int lds_bytes);
+
+}  // namespace qldpc

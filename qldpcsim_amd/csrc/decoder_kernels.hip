@@ -1,0 +1,400 @@
+// decoder_kernels.hip — batched BP / normalized Min-Sum decoding on MI355X (gfx950).
+//
+// Replaces the per-shot message loops of albertogp71/qLDPCsim
+//   MS_decoder  qLDPCsim/decoders.py:110-182
+//   BP_decoder  qLDPCsim/decoders.py:189-290
+// for a batch of syndromes (one "half-shot" = one decode of one syndrome).
+//
+// Execution model:
+//  * One wavefront decodes one half-shot start to finish. All of its message
+//    state lives in that wave's slice of LDS:
+//        post  f64[n]          posterior LLR per variable  (decoders.py:173 / :276)
+//        c2v   f32[E] (MS) or f64[E] (BP), stored in CSC (variable-major) order
+//        syn / parity bit-words (layered schedule only)
+//    so HBM traffic is the syndrome in (m B), ê out (n B), iterations/flags.
+//  * The Tanner graph (CSR check->(var, csc position), CSC pointers, layer
+//    lists) is one read-only blob staged into LDS once per workgroup.
+//  * Check-node phase: lane owns whole checks; min1/min2/first-argmin/sign
+//    product (MS) or the tanh product (BP) are folded in-lane over the
+//    check's edges in ascending variable order — no cross-lane traffic.
+//  * Variable-node phase: lane owns whole variables; the column sum runs over
+//    the contiguous CSC segment in ascending check order — the exact order of
+//    NumPy's axis-0 reduction (MS, float32) or np.sum's pairwise rule (BP).
+//  * Persistent: each wave strides over half-shots; the grid is sized to the
+//    occupancy the LDS budget allows (host side, capi.cpp).
+//
+// Numerics: MS c2v = fl32(beta * min) formed in float64;
+// VN sum float32 sequential; posterior and v2c float64; first layer of the
+// first iteration sees float32(L). BP float64 with device tanh/atanh.
+// Compiled with -ffp-contract=off: no FMA contraction may change a rounding.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "decoder_kernels.h"
+
+namespace qldpc {
+
+__device__ __forceinline__ void wave_sync() {
+  // Lanes of one wave exchange data through LDS between phases. DS
+  // instructions of a wave complete in order; the fences only stop the
+  // compiler from moving LDS accesses across the phase boundary.
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint64_t ballot(int pred) { return __ballot(pred); }
+
+// NumPy DOUBLE_pairwise_sum over a contiguous LDS segment (np.sum of a 1-D
+// float64 array = 0.0 + pairwise(all); decoders.py:269, :276). n <= 128.
+__device__ __forceinline__ double np_pairwise_sum(const double* a, int n) {
+  if (n < 8) {
+    double res = -0.0;
+    for (int i = 0; i < n; ++i) res += a[i];
+    return 0.0 + res;
+  }
+  double r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
+  int i = 8;
+  const int nb = n - (n % 8);
+  for (; i < nb; i += 8) {
+    r0 += a[i + 0]; r1 += a[i + 1]; r2 += a[i + 2]; r3 += a[i + 3];
+    r4 += a[i + 4]; r5 += a[i + 5]; r6 += a[i + 6]; r7 += a[i + 7];
+  }
+  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (; i < n; ++i) res += a[i];
+  return 0.0 + res;
+}
+
+// Set bit `c` of a per-wave bit-word array for every lane whose predicate is
+// true, for a chunk of 64 consecutive indices starting at c0 (all lanes call).
+__device__ __forceinline__ void store_bits64(uint32_t* words, int c0, int pred, int lane) {
+  const uint64_t b = ballot(pred);
+  if (lane == 0) words[c0 >> 5] = (uint32_t)b;
+  if (lane == 1) words[(c0 >> 5) + 1] = (uint32_t)(b >> 32);
+}
+
+struct LdsView {
+  const uint32_t* cn_tab;   // [E] (relabeled var << 16) | csc position, CSR edge order
+  const uint16_t* row_ptr;  // [m+1]
+  const uint16_t* vn_ptr;   // [n+1]
+  const uint16_t* vn_chk;   // [E]   check of each CSC position (layered)
+  const uint16_t* lay_ptr;  // [L+1]
+  const uint16_t* lay_rows; // [*]
+  const uint16_t* adj_ptr;  // [L+1]
+  const uint16_t* adj_vars; // [*]
+};
+
+// ---------------------------------------------------------------------------
+// Check-node update of one check `c` (lane-local).
+//   MS: decoders.py:155-169.  BP: decoders.py:249-262.
+// Returns the check's current parity XOR syndrome bit ("unsatisfied"),
+// computed from the hard decisions of the posteriors it reads (only
+// meaningful when !first).
+// ---------------------------------------------------------------------------
+template <int ALGO, int DC>
+__device__ __forceinline__ uint32_t cn_update(const DecodeArgs& a, const LdsView& g, int c,
+                                              uint32_t synb, bool first, const double* post,
+                                              void* c2v_raw, int& fl) {
+  const int e0 = DC ? c * DC : (int)g.row_ptr[c];
+  const int deg = DC ? DC : (int)g.row_ptr[c + 1] - e0;
+  uint32_t par = 0;
+  if constexpr (ALGO == ALGO_MS) {
+    float* c2v = (float*)c2v_raw;
+    double min1 = __builtin_inf(), min2 = __builtin_inf();
+    int idx = 0;
+    uint32_t negm = 0;
+    const double vfirst = (double)a.L32;
+#pragma unroll
+    for (int k = 0; k < (DC ? DC : 32); ++k) {
+      if (!DC && k >= deg) break;
+      const uint32_t t = g.cn_tab[e0 + k];
+      const int j = (int)(t >> 16), pos = (int)(t & 0xffffu);
+      double v;
+      if (first) {
+        v = vfirst;                                   // float32(L) (:148-149)
+      } else {
+        const double pj = post[j];
+        par ^= (uint32_t)(pj < 0.0);                  // hard decision (:174)
+        v = pj - (double)c2v[pos];                    // v2c = post - c2v (:177)
+      }
+      negm |= (uint32_t)(v < 0.0) << k;              // np.sign, 0 -> +1 (:157-158)
+      const double av = __builtin_fabs(v);
+      idx = (av < min1) ? k : idx;                   // first argmin (:161)
+      min2 = __builtin_fmin(min2, __builtin_fmax(min1, av));  // min of the rest (:162-164)
+      min1 = __builtin_fmin(min1, av);
+    }
+    if (deg == 0) return synb;                       // no edges: c2v stays 0
+    if (__builtin_isinf(min1)) min1 = 0.0;           // (:165)
+    if (__builtin_isinf(min2)) min2 = 0.0;           // (:166)
+    if (min1 == 0.0) fl |= FLAG_MIN_ZERO;            // App. A.1.6 leak case (flagged, not emulated)
+    const uint32_t negprod = (uint32_t)(__builtin_popcount(negm) & 1) ^ synb;
+    // c2v_e = fl32(beta * syn * prod * min_e / sign_e): magnitude rounded from
+    // the float64 product once, sign = syn * prod * sign_e (:167-168).
+    const float c1 = (float)(a.beta * min1), c2 = (float)(a.beta * min2);
+#pragma unroll
+    for (int k = 0; k < (DC ? DC : 32); ++k) {
+      if (!DC && k >= deg) break;
+      const int pos = (int)(g.cn_tab[e0 + k] & 0xffffu);
+      const float mag = (k == idx) ? c2 : c1;
+      c2v[pos] = (((negm >> k) & 1u) ^ negprod) ? -mag : mag;
+    }
+  } else {
+    double* c2v = (double*)c2v_raw;
+    if (deg == 0) return synb;                       // `continue` (:251-252)
+    double prod = 1.0;
+#pragma unroll
+    for (int k = 0; k < (DC ? DC : 32); ++k) {
+      if (!DC && k >= deg) break;
+      const uint32_t t = g.cn_tab[e0 + k];
+      const int j = (int)(t >> 16), pos = (int)(t & 0xffffu);
+      const double pj = post[j];
+      par ^= (uint32_t)(pj < 0.0);
+      const double v = pj - c2v[pos];                // v2c (:269)
+      const double th = tanh(v / 2.0);               // (:254)
+      prod *= th;                                    // np.prod: sequential fold
+      c2v[pos] = th;                                 // scratch: own edge, rewritten below
+    }
+    if (!DC && deg > 32) {
+      // generic degrees > 32: second half of the fold (rare; bicycle = 18)
+      for (int k = 32; k < deg; ++k) {
+        const uint32_t t = g.cn_tab[e0 + k];
+        const int j = (int)(t >> 16), pos = (int)(t & 0xffffu);
+        const double pj = post[j];
+        par ^= (uint32_t)(pj < 0.0);
+        const double th = tanh((pj - c2v[pos]) / 2.0);
+        prod *= th;
+        c2v[pos] = th;
+      }
+    }
+    const double lim = 1.0 - a.eps;
+    for (int k = 0; k < deg; ++k) {
+      const int pos = (int)(g.cn_tab[e0 + k] & 0xffffu);
+      const double th = c2v[pos];
+      if (th == 0.0) fl |= FLAG_NONFINITE;
+      double th2 = prod / th;                        // (:256)
+      if (__builtin_fabs(th2) >= lim)                // (:257-258)
+        th2 = th2 - a.eps * (th2 > 0.0 ? 1.0 : (th2 < 0.0 ? -1.0 : 0.0));
+      double val = 2.0 * atanh(th2);                 // (:259)
+      if (synb) val = -val;                          // (:260-261)
+      if (!__builtin_isfinite(val)) fl |= FLAG_NONFINITE;
+      c2v[pos] = val;
+    }
+  }
+  return par ^ synb;
+}
+
+// Variable-node update of relabeled variable j: column sum in ascending check
+// order. MS: float32 sequential (np.sum axis=0, decoders.py:172), post = L +
+// (f64)S (:173). BP: np.sum pairwise rule, post = L0 + S (:269, :276).
+template <int ALGO>
+__device__ __forceinline__ double vn_post(const DecodeArgs& a, const LdsView& g, int j,
+                                          const void* c2v_raw) {
+  const int p0 = g.vn_ptr[j], p1 = g.vn_ptr[j + 1];
+  if constexpr (ALGO == ALGO_MS) {
+    const float* c2v = (const float*)c2v_raw;
+    float s = 0.0f;
+    for (int p = p0; p < p1; ++p) s += c2v[p];
+    return a.L + (double)s;
+  } else {
+    const double* c2v = (const double*)c2v_raw;
+    if (p1 == p0) return a.L;                        // L_post[j] = L0 (:277-278)
+    return a.L + np_pairwise_sum(c2v + p0, p1 - p0);
+  }
+}
+
+template <int ALGO, bool LAYERED, int DC>
+__global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+
+  // Stage the read-only graph blob into LDS (16-byte vector copies).
+  {
+    const uint4* src = (const uint4*)a.blob;
+    uint4* dst = (uint4*)lds;
+    const int nvec = a.blob_bytes >> 4;
+    for (int i = threadIdx.x; i < nvec; i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+
+  LdsView g;
+  g.cn_tab = (const uint32_t*)(lds + a.off_cn_tab);
+  g.row_ptr = (const uint16_t*)(lds + a.off_row_ptr);
+  g.vn_ptr = (const uint16_t*)(lds + a.off_vn_ptr);
+  g.vn_chk = (const uint16_t*)(lds + a.off_vn_chk);
+  g.lay_ptr = (const uint16_t*)(lds + a.off_lay_ptr);
+  g.lay_rows = (const uint16_t*)(lds + a.off_lay_rows);
+  g.adj_ptr = (const uint16_t*)(lds + a.off_adj_ptr);
+  g.adj_vars = (const uint16_t*)(lds + a.off_adj_vars);
+
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int waves = blockDim.x >> 6;
+  unsigned char* ws = lds + a.blob_bytes + wid * a.wave_bytes;
+  double* post = (double*)ws;
+  void* c2v = (void*)(ws + a.off_c2v);
+  uint32_t* synw = (uint32_t*)(ws + a.off_synw);
+  uint32_t* parw = (uint32_t*)(ws + a.off_parw);
+
+  const int m = a.m, n = a.n;
+  const int nwords = (m + 31) >> 5;
+
+  for (long long hs = (long long)blockIdx.x * waves + wid; hs < a.batch;
+       hs += (long long)gridDim.x * waves) {
+    const uint8_t* syn = a.syn + hs * (long long)m;
+    int fl = 0;
+    int iters = a.max_iter;
+    bool conv = false;
+
+    if constexpr (!LAYERED) {
+      // ---------------- flooding: one layer holding every check ------------
+      uint32_t synreg = 0;  // bit i = syndrome of check lane + 64 i
+      for (int i = 0, c = lane; c < m; ++i, c += 64) synreg |= (uint32_t)(syn[c] & 1) << i;
+      for (int it = 0;; ++it) {
+        // CN over all checks; its parity pass is the stop test of iteration it-1
+        // (decoders.py:175-176 — checks read the posteriors the last VN wrote).
+        uint32_t unsat = 0;
+        for (int i = 0, c = lane; c < m; ++i, c += 64)
+          unsat |= cn_update<ALGO, DC>(a, g, c, (synreg >> i) & 1u, it == 0, post, c2v, fl);
+        if (it > 0 && ballot(unsat != 0) == 0) {
+          iters = it;
+          conv = true;
+          break;
+        }
+        wave_sync();
+        for (int j = lane; j < n; j += 64) post[j] = vn_post<ALGO>(a, g, j, c2v);
+        wave_sync();
+        if (it + 1 == a.max_iter) {
+          // final stop test after the last VN (its result only sets the flag:
+          // both branches of the reference return max_iter, :176 / :182)
+          uint32_t un = 0;
+          for (int i = 0, c = lane; c < m; ++i, c += 64) {
+            const int e0 = DC ? c * DC : (int)g.row_ptr[c];
+            const int deg = DC ? DC : (int)g.row_ptr[c + 1] - e0;
+            uint32_t par = 0;
+            for (int k = 0; k < deg; ++k) par ^= (uint32_t)(post[g.cn_tab[e0 + k] >> 16] < 0.0);
+            un |= par ^ ((synreg >> i) & 1u);
+          }
+          conv = ballot(un != 0) == 0;
+          break;
+        }
+      }
+    } else {
+      // ---------------- layered / serial: explicit row lists ----------------
+      // State starts at c2v = 0, post = L (msg_v2c = L, :148-149 / :235).
+      const double L = a.L;
+      for (int j = lane; j < n; j += 64) post[j] = L;
+      if constexpr (ALGO == ALGO_MS) {
+        float* c = (float*)c2v;
+        for (int p = lane; p < a.E; p += 64) c[p] = 0.0f;
+      } else {
+        double* c = (double*)c2v;
+        for (int p = lane; p < a.E; p += 64) c[p] = 0.0;
+      }
+      // syndrome bits and the parity of the initial hard decisions (all = L<0)
+      for (int c0 = 0; c0 < m; c0 += 64) {
+        const int c = c0 + lane;
+        const int in = c < m;
+        store_bits64(synw, c0, in ? (syn[c] & 1) : 0, lane);
+        int deg = 0;
+        if (in) deg = DC ? DC : (int)g.row_ptr[c + 1] - (int)g.row_ptr[c];
+        store_bits64(parw, c0, in && (L < 0.0) && (deg & 1), lane);
+      }
+      wave_sync();
+      bool first = true;
+      for (int it = 0; it < a.max_iter && !conv; ++it) {
+        for (int l = 0; l < a.n_layers; ++l) {
+          // CN over the layer's rows (Jacobi: all read the same posteriors)
+          const int q0 = g.lay_ptr[l], q1 = g.lay_ptr[l + 1];
+          for (int q = q0 + lane; q < q1; q += 64) {
+            const int c = g.lay_rows[q];
+            const uint32_t sb = (synw[c >> 5] >> (c & 31)) & 1u;
+            (void)cn_update<ALGO, DC>(a, g, c, sb, first, post, c2v, fl);
+          }
+          first = false;
+          wave_sync();
+          // VN over the variables adjacent to the layer (others are unchanged,
+          // so recomputing every column as decoders.py:172 / :265 does is
+          // bit-identical); hard-decision flips toggle check parities.
+          const int v0 = g.adj_ptr[l], v1 = g.adj_ptr[l + 1];
+          for (int q = v0 + lane; q < v1; q += 64) {
+            const int j = g.adj_vars[q];
+            const double old = post[j];
+            const double nw = vn_post<ALGO>(a, g, j, c2v);
+            post[j] = nw;
+            if ((old < 0.0) != (nw < 0.0)) {
+              for (int p = g.vn_ptr[j]; p < g.vn_ptr[j + 1]; ++p) {
+                const int c = g.vn_chk[p];
+                atomicXor(&parw[c >> 5], 1u << (c & 31));
+              }
+            }
+          }
+          wave_sync();
+          // stop test after every layer (:175-176 / :283-285)
+          uint32_t un = 0;
+          for (int w = lane; w < nwords; w += 64) un |= parw[w] ^ synw[w];
+          if (ballot(un != 0) == 0) {
+            iters = it + 1;
+            conv = true;
+            break;
+          }
+        }
+      }
+    }
+
+    // ---------------- outputs (original column order) ----------------------
+    uint8_t* eh = a.ehat + hs * (long long)n;
+    double* po = a.post ? a.post + hs * (long long)n : nullptr;
+    for (int jo = lane; jo < n; jo += 64) {
+      const double pv = post[a.vinv[jo]];
+      eh[jo] = (uint8_t)(pv < 0.0);                  // e_hat = post < 0 (:174 / :280)
+      if (po) po[jo] = pv;
+    }
+    // OR the lane-local flags across the wave
+    uint32_t fall = 0;
+    {
+      const uint64_t b1 = ballot((fl & FLAG_MIN_ZERO) != 0);
+      const uint64_t b2 = ballot((fl & FLAG_NONFINITE) != 0);
+      fall = (b1 ? FLAG_MIN_ZERO : 0) | (b2 ? FLAG_NONFINITE : 0) | (conv ? FLAG_CONVERGED : 0);
+    }
+    if (lane == 0) {
+      a.iters[hs] = iters;
+      if (a.flags) a.flags[hs] = (int32_t)fall;
+    }
+    wave_sync();  // the next half-shot reuses this wave's LDS slice
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host-side launch helpers (called from capi.cpp)
+// ---------------------------------------------------------------------------
+template <int ALGO, bool LAYERED, int DC>
+static const void* kernel_ptr() {
+  return (const void*)&decode_kernel<ALGO, LAYERED, DC>;
+}
+
+const void* select_kernel(int algo, bool layered, int dc) {
+#define QLDPC_PICK(ALG)                                                                 \
+  switch (dc) {                                                                         \
+    case 7: return layered ? kernel_ptr<ALG, true, 7>() : kernel_ptr<ALG, false, 7>();  \
+    case 8: return layered ? kernel_ptr<ALG, true, 8>() : kernel_ptr<ALG, false, 8>();  \
+    default: return layered ? kernel_ptr<ALG, true, 0>() : kernel_ptr<ALG, false, 0>(); \
+  }
+  if (algo == ALGO_MS) {
+    QLDPC_PICK(ALGO_MS)
+  } else {
+    QLDPC_PICK(ALGO_BP)
+  }
+#undef QLDPC_PICK
+}
+
+hipError_t launch_decode(const void* kernel, const DecodeArgs& args, int grid, int block,
+                         int lds_bytes, hipStream_t stream) {
+  void* params[] = {(void*)&args};
+  return hipLaunchKernel(kernel, dim3(grid), dim3(block), params, (size_t)lds_bytes, stream);
+}
+
+hipError_t configure_kernel(const void* kernel, int lds_bytes) {
+  return hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+}
+
+}  // namespace qldpc

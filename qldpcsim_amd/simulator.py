@@ -1,0 +1,251 @@
+"""Monte-Carlo driver with the reference simulator's API, batched on the GPU.
+
+Same names, arguments, flags and counters as albertogp71/qLDPCsim
+qLDPCsim/simulator.py:
+    load_matrix(path)                                   simulator.py:20-35
+    simulate_p(Hx, Hz, p, shots, decType, decIterations,
+               decSchedule, OSDorder, rngSeed) -> dict  simulator.py:167-315
+    simulate(HxFile, HzFile, p, shots, ...)             simulator.py:319-347
+    main(argv)                                          simulator.py:351-373
+
+What changes underneath: instead of a serial Python loop over shots
+(simulator.py:244-304) the shots are processed in batches — one kernel
+launch per half (X: Hz with the Hx-derived layers; Z: Hx with the
+Hz-derived layers, the reference's cross-wiring, :278-282) — and the counters
+are formed with array operations with the reference's exact definitions.
+With torch.distributed initialised, shots shard across ranks and the six
+counters are summed with one all_reduce (RCCL over xGMI on the GPU node).
+
+Syndrome source: Stim is not available in this environment,
+so shots come from a per-qubit Pauli sampler (X, Y, Z each p/3 — the
+circuit's PAULI_CHANNEL_1(p/3,p/3,p/3), simulator.py:107) whose statistics
+equal the circuit's. `rngSeed` seeds it (the reference
+seeds np.random, which its unseeded Stim sampler never reads: runs there are
+not reproducible; here they are).
+"""
+import argparse
+import sys
+import time
+from typing import Optional
+
+import numpy as np
+
+from . import decoders
+from .schedule import layerize, select_layers, pack_layers  # noqa: F401  (re-exported)
+
+__all__ = ["load_matrix", "simulate_p", "simulate", "main", "layerize", "sample_channel",
+           "count_outcomes"]
+
+COUNTER_KEYS = ("DecFailures_X", "DecFailures_Z", "decSuccessExact", "decSuccessDegen",
+                "nIterAccX", "nIterAccZ")
+
+
+def load_matrix(path: str) -> np.ndarray:
+    """Load a binary matrix from .npy or whitespace text (simulator.py:20-35)."""
+    if path.endswith(".npy"):
+        mat = np.load(path, allow_pickle=False)
+    else:
+        mat = []
+        with open(path, "rt") as f:
+            for line in f:
+                line = line.strip()
+                if not line:
+                    continue
+                mat.append([int(x) for x in line.split()])
+        mat = np.array(mat, dtype=int)
+    return (mat % 2).astype(np.int8)
+
+
+def sample_channel(Hx, Hz, p, shots, rng):
+    """Depolarizing-channel samples in the circuit's output layout.
+
+    Returns (sy_z, sy_x, errX, errZ) as uint8 arrays ([shots, m_z], [shots, m_x],
+    [shots, n], [shots, n]) — the slices simulator.py:249-252 takes of a Stim
+    sample row [sy_z | sy_x | errX | errZ].
+    """
+    n = Hx.shape[1]
+    u = rng.random((shots, n), dtype=np.float32)
+    q = np.float32(p / 3)
+    X = u < q
+    Y = (u >= q) & (u < 2 * q)
+    Z = (u >= 2 * q) & (u < np.float32(p))
+    errX = (X | Y).astype(np.uint8)
+    errZ = (Z | Y).astype(np.uint8)
+    # H·e mod 2 via a float32 product (exact: row weights << 2^24)
+    sy_z = (errX.astype(np.float32) @ Hz.T.astype(np.float32)).astype(np.int64) % 2
+    sy_x = (errZ.astype(np.float32) @ Hx.T.astype(np.float32)).astype(np.int64) % 2
+    return sy_z.astype(np.uint8), sy_x.astype(np.uint8), errX, errZ
+
+
+def count_outcomes(Hx, Hz, sy_z, sy_x, errX, errZ, eX, eZ, itX, itZ):
+    """The reference's per-shot outcome counting (simulator.py:291-303), vectorised.
+
+    exact:  errX == eX_hat and errZ == eZ_hat                       (:294-295)
+    degen:  otherwise, Hz @ (errX ^ eX_hat) == 0 and Hx @ (errZ ^ eZ_hat) == 0
+            over the integers, no mod 2 (:296-298; the reference also calls
+            breakpoint() there)
+    failX/Z: syndrome of the estimate differs from the measured one (:300-303)
+    """
+    exact = np.all(errX == eX, axis=1) & np.all(errZ == eZ, axis=1)
+    dX = (errX ^ eX).astype(np.float32)
+    dZ = (errZ ^ eZ).astype(np.float32)
+    degen = (~exact) & np.all(dX @ Hz.T.astype(np.float32) == 0, axis=1) & \
+        np.all(dZ @ Hx.T.astype(np.float32) == 0, axis=1)
+    sX = (eX.astype(np.float32) @ Hz.T.astype(np.float32)).astype(np.int64) % 2
+    sZ = (eZ.astype(np.float32) @ Hx.T.astype(np.float32)).astype(np.int64) % 2
+    failX = np.any(sX != sy_z, axis=1)
+    failZ = np.any(sZ != sy_x, axis=1)
+    return {
+        "DecFailures_X": int(failX.sum()),
+        "DecFailures_Z": int(failZ.sum()),
+        "decSuccessExact": int(exact.sum()),
+        "decSuccessDegen": int(degen.sum()),
+        "nIterAccX": int(np.asarray(itX, dtype=np.int64).sum()),
+        "nIterAccZ": int(np.asarray(itZ, dtype=np.int64).sum()),
+    }
+
+
+def _dist():
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return dist, dist.get_rank(), dist.get_world_size()
+    except ImportError:
+        pass
+    return None, 0, 1
+
+
+def simulate_p(Hx: np.ndarray, Hz: np.ndarray, p: float, shots: int = 1000, decType: str = "MS",
+               decIterations: int = 99, decSchedule: str = "F", OSDorder: int = -1,
+               rngSeed: Optional[int] = None, *, batch_size: int = 1 << 16,
+               verbose: bool = True, samples=None) -> dict:
+    """One depolarizing probability: sample, decode both halves, count.
+
+    Returns the reference's dict (simulator.py:308-315). `samples`, if given,
+    is a tuple (sy_z, sy_x, errX, errZ) to decode instead of sampling (used by
+    the parity tests). Extra keyword arguments default to reference behaviour.
+    """
+    if rngSeed is not None:
+        np.random.seed(rngSeed)                    # reference side effect (:187-188)
+    dist, rank, world = _dist()
+    m_z = Hz.shape[0] if Hz.size else 0
+    m_x = Hx.shape[0] if Hx.size else 0
+    n = Hx.shape[1]
+    if Hz.size and Hz.shape[1] != n:
+        raise ValueError("Hx and Hz must have the same number of columns (physical qubits).")
+    layersX, layersZ = select_layers(Hx, Hz, decSchedule)   # raises ValueError (:236)
+    if decType in ("NG", "BF"):
+        raise NotImplementedError(
+            f"decType {decType!r} (decoders.py NG_decoder/BF_decoder) is outside the MI355X "
+            "decoder's scope (SURVEY.md §2 rows 4-5); use 'MS' or 'BP'")
+    if decType not in ("MS", "BP"):
+        raise ValueError("Unrecognized decoder type.")
+    # the reference never passes OSDorder to BP_decoder (:281-282)
+    osd = OSDorder if decType == "MS" else -1
+    lpX, lrX = pack_layers(layersX, Hz.shape[0])    # X half decodes Hz with Hx's layers
+    lpZ, lrZ = pack_layers(layersZ, Hx.shape[0])    # Z half decodes Hx with Hz's layers
+
+    # this rank's share of the shots
+    my_shots = shots // world + (1 if rank < shots % world else 0)
+    seed = None if rngSeed is None else [int(rngSeed), int(rank)]
+    rng = np.random.default_rng(seed)
+    tot = {k: 0 for k in COUNTER_KEYS}
+    t0 = time.time()
+    done = 0
+    while done < my_shots:
+        B = min(batch_size, my_shots - done)
+        if samples is not None:
+            sl = slice(done, done + B)
+            sy_z, sy_x, errX, errZ = (np.asarray(a)[sl].astype(np.uint8) for a in samples)
+        else:
+            sy_z, sy_x, errX, errZ = sample_channel(Hx, Hz, p, B, rng)
+        rX = decoders.decode_batch(Hz, sy_z, p / 3, decIterations, algo=decType, osd_order=osd,
+                                   layer_ptr=lpX, layer_rows=lrX)
+        rZ = decoders.decode_batch(Hx, sy_x, p / 3, decIterations, algo=decType, osd_order=osd,
+                                   layer_ptr=lpZ, layer_rows=lrZ)
+        c = count_outcomes(Hx, Hz, sy_z, sy_x, errX, errZ, rX.ehat, rZ.ehat, rX.iters, rZ.iters)
+        for k in tot:
+            tot[k] += c[k]
+        done += B
+        if verbose and rank == 0:
+            print(f"\r(p={p:5.2e}) Decoding block n. {done:3}/{my_shots:4}... "
+                  f"Dec. failure rates (X,Z): {tot['DecFailures_X'] / done:.2e}, "
+                  f"{tot['DecFailures_Z'] / done:.2e} ({done / (time.time() - t0):.3g} shots/s)",
+                  end="", flush=True)
+    if dist is not None and world > 1:
+        import torch
+        backend = dist.get_backend()
+        dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([tot[k] for k in COUNTER_KEYS], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)   # the sweep's only collective
+        tot = dict(zip(COUNTER_KEYS, (int(v) for v in t.cpu().tolist())))
+    if verbose and rank == 0:
+        print()
+    return {
+        "DecFailures_X": tot["DecFailures_X"],
+        "DecFailures_Z": tot["DecFailures_Z"],
+        "decSuccessExact": tot["decSuccessExact"],
+        "decSuccessDegen": tot["decSuccessDegen"],
+        "Avg_number_of_iterations_X": tot["nIterAccX"] / float(shots),
+        "Avg_number_of_iterations_Z": tot["nIterAccZ"] / float(shots),
+    }
+
+
+def format_results(p, results, shots):
+    """The reference's results table (simulator.py:342-347)."""
+    lines = ["\n                             ===          SIMULATION RESULTS          ===\n",
+             "   Depolarizing probability | qBlock error rate | Decoding failures (X,Z) | Average iterations (X,Z)",
+             "----------------------------+-------------------+-------------------------+---------------------------"]
+    for pT, r in zip(p, results):
+        qbler = 1. - (r["decSuccessExact"] + r["decSuccessDegen"]) / shots
+        lines.append(f"         {pT:10.2e}         |     {qbler:7.2e}      |       "
+                     f"{r['DecFailures_X']:5},{r['DecFailures_Z']:5}       |      "
+                     f"{r['Avg_number_of_iterations_X']:5.2f}, {r['Avg_number_of_iterations_Z']:5.2f}")
+    return "\n".join(lines)
+
+
+def simulate(HxFile: str, HzFile: str, p, shots: int = 1000, decType: str = "MS",
+             decIterations: int = 99, decSchedule: str = "F", OSDorder: int = -1,
+             rngSeed: Optional[int] = None, *, batch_size: int = 1 << 16, verbose: bool = True,
+             return_results: bool = False):
+    """p-sweep + results table (simulator.py:319-347). Returns None like the
+    reference unless return_results=True."""
+    Hx = load_matrix(HxFile)
+    Hz = load_matrix(HzFile)
+    assert max(p) <= 1. and min(p) >= 0.
+    results = []
+    for pT in p:
+        results.append(simulate_p(Hx, Hz, p=pT, shots=shots, rngSeed=rngSeed, decType=decType,
+                                  decIterations=decIterations, decSchedule=decSchedule,
+                                  OSDorder=OSDorder, batch_size=batch_size, verbose=verbose))
+    _, rank, _ = _dist()
+    if rank == 0:
+        print(format_results(p, results, shots))
+    return results if return_results else None
+
+
+def main(argv=None):
+    parser = argparse.ArgumentParser(description="Stim-based QC-LDPC depolarizing-channel simulator.")
+    parser.add_argument("--Hx", required=True, help="Path to Hx parity-check matrix (.npy).")
+    parser.add_argument("--Hz", required=True, help="Path to Hz parity-check matrix (.npy).")
+    parser.add_argument("--p", type=float, nargs="+", required=True, help="Depolarizing probability.")
+    parser.add_argument("--shots", type=int, default=1000, help="Number of Monte Carlo shots.")
+    parser.add_argument("--rngSeed", type=int, default=None, help="RNG seed.")
+    parser.add_argument("--decType", choices=["NG", "BF", "MS", "BP"], default="MS",
+                        help="Decoder type: [NG] Naive Greedy; [MS] Min-Sum; [BP] Belief Propagation.")
+    parser.add_argument("--decIterations", type=int, default=99, help="Number of decoding iterations.")
+    parser.add_argument("--decSchedule", choices=["F", "L", "S"], default="F",
+                        help="Decoder scheduling method: [F] flooding; [L] layered; [S] serial.")
+    parser.add_argument("--OSDorder", type=int, default=-1, help="Ordered Statistics Decoding order.")
+    parser.add_argument("--batch", type=int, default=1 << 16, help="Shots per GPU batch.")
+    args = parser.parse_args(argv)
+    print("\n   Command line arguments:")
+    print(args)
+    print("")
+    simulate(HxFile=args.Hx, HzFile=args.Hz, p=args.p, shots=args.shots, decType=args.decType,
+             decIterations=args.decIterations, decSchedule=args.decSchedule,
+             OSDorder=args.OSDorder, rngSeed=args.rngSeed, batch_size=args.batch)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

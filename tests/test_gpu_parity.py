@@ -1,0 +1,169 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the reference's golden
+vectors and the pinned CPU oracle on identical syndromes.
+
+Bar:
+  MS — hard decisions, iteration counts and float64 posteriors bit-exact.
+  BP — iteration counts and hard decisions exact; posteriors within
+       rtol 1e-5 (north-star tolerance; device tanh/atanh differ from
+       glibc/NumPy by ULPs).
+"""
+import numpy as np
+import pytest
+
+from conftest import golden_cases, half_matrix
+
+pytestmark = pytest.mark.gpu
+
+BP_RTOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def dec():
+    from qldpcsim_amd import _lib, decoders
+    if _lib.device_count() < 1:
+        pytest.fail("no HIP device visible: the GPU tests must run on the MI355X box")
+    return decoders
+
+
+CASES = [(c, a) for c, a in golden_cases() if "raises" not in c and c["osd"] < 0]
+OSD_CASES = [(c, a) for c, a in golden_cases("_osd")]
+RAISE_CASES = [(c, a) for c, a in golden_cases() if c.get("raises") == "IndexError"]
+
+
+def _id(ca):
+    c = ca[0]
+    return f"{c['algo']}-{c['code']}-{c['half']}-{c['sched']}-{c['kind']}-p{c['p_phys']}-it{c['max_iter']}"
+
+
+def _assert_post(algo, got, want):
+    if algo == "MS":
+        np.testing.assert_array_equal(got.view(np.uint64), want.view(np.uint64))
+    else:
+        np.testing.assert_allclose(got, want, rtol=BP_RTOL, atol=0)
+
+
+@pytest.mark.parametrize("ca", CASES, ids=[_id(x) for x in CASES])
+def test_kernel_matches_reference_golden(dec, ca):
+    c, a = ca
+    H = half_matrix(c)
+    r = dec.decode_batch(H, a["syn"], c["p_phys"] / 3, c["max_iter"], algo=c["algo"],
+                         want_post=True, layer_ptr=a["layer_ptr"], layer_rows=a["layer_rows"])
+    np.testing.assert_array_equal(r.iters, a["iters"])
+    np.testing.assert_array_equal(r.ehat, a["ehat"])
+    _assert_post(c["algo"], r.post, a["post"])
+    assert not np.any(r.flags & 2), "min-sum zero-message leak case hit"
+
+
+@pytest.mark.parametrize("ca", OSD_CASES, ids=[_id(x) + f"-osd{x[0]['osd']}" for x in OSD_CASES])
+def test_dropin_shims_with_osd_match_reference(dec, ca):
+    c, a = ca
+    H = half_matrix(c)
+    fn = dec.MS_decoder if c["algo"] == "MS" else dec.BP_decoder
+    for k in range(a["syn"].shape[0]):
+        lp, lr = a["layer_ptr"], a["layer_rows"]
+        layers = [lr[lp[i]:lp[i + 1]] for i in range(len(lp) - 1)]
+        e, it = fn(H, a["syn"][k].astype(int), c["p_phys"] / 3, max_iter=c["max_iter"],
+                   layers=layers, OSDorder=c["osd"])
+        assert it == a["iters"][k]
+        np.testing.assert_array_equal(e.astype(np.uint8), a["ehat"][k])
+        assert e.dtype == (np.int8 if c["algo"] == "MS" else np.int64)
+
+
+@pytest.mark.parametrize("ca", RAISE_CASES[:4], ids=[_id(x) for x in RAISE_CASES[:4]])
+def test_out_of_range_layers_raise_indexerror(dec, ca):
+    c, _ = ca
+    from qldpcsim_amd import codes, schedule
+    Hx, Hz = codes.load_code(c["code"])
+    lx, lz = schedule.select_layers(Hx, Hz, c["sched"])
+    H, layers = (Hz, lx) if c["half"] == "X" else (Hx, lz)
+    with pytest.raises(IndexError):
+        dec.MS_decoder(H, np.ones(H.shape[0], int), 0.01, max_iter=2, layers=layers)
+
+
+# ---------------------------------------------------------------------------
+# larger batches against the oracle (same seeded syndromes)
+# ---------------------------------------------------------------------------
+def _channel(Hx, Hz, p, B, seed):
+    rng = np.random.default_rng(seed)
+    n = Hx.shape[1]
+    u = rng.random((B, n))
+    X, Y, Z = u < p / 3, (u >= p / 3) & (u < 2 * p / 3), (u >= 2 * p / 3) & (u < p)
+    ex, ez = (X | Y).astype(np.float32), (Z | Y).astype(np.float32)
+    sz = (ex @ Hz.T.astype(np.float32)).astype(np.int64) % 2
+    sx = (ez @ Hx.T.astype(np.float32)).astype(np.int64) % 2
+    return sz.astype(np.uint8), sx.astype(np.uint8)
+
+
+@pytest.mark.parametrize("code,sched,algo,p,max_iter,B", [
+    ("LP118_0", "F", "MS", None, 50, 4096),      # headline config, random (fixed-work) syndromes
+    ("LP118_0", "F", "MS", 0.05, 50, 4096),
+    ("LP118_2", "L", "MS", 0.05, 50, 2048),
+    ("LP04_0", "S", "MS", 0.08, 20, 1024),
+    ("LP04_0", "F", "MS", 0.1, 50, 4096),
+    ("LP118_0", "F", "BP", 0.05, 100, 512),
+    ("LP118_0", "L", "BP", 0.05, 100, 256),
+    ("bicycle", "F", "BP", 0.05, 30, 256),
+])
+def test_kernel_matches_oracle_batches(dec, code, sched, algo, p, max_iter, B):
+    from oracle import oracle
+    from qldpcsim_amd import codes, schedule
+    Hx, Hz = codes.load_code(code)
+    lx, lz = schedule.select_layers(Hx, Hz, sched)
+    prior = (p if p is not None else 0.05) / 3
+    if p is None:
+        rng = np.random.default_rng(20251226)
+        sz = rng.integers(0, 2, (B, Hz.shape[0]), dtype=np.uint8)
+        sx = rng.integers(0, 2, (B, Hx.shape[0]), dtype=np.uint8)
+    else:
+        sz, sx = _channel(Hx, Hz, p, B, 7)
+    for H, layers, syn in ((Hz, lx, sz), (Hx, lz, sx)):
+        lp, lr = schedule.pack_layers(layers, H.shape[0])
+        r = dec.decode_batch(H, syn, prior, max_iter, algo=algo, want_post=True,
+                             layer_ptr=lp, layer_rows=lr)
+        e, it, post, fl = oracle.decode_batch(algo, H, syn, prior, max_iter, lp, lr)
+        if algo == "MS":
+            np.testing.assert_array_equal(r.iters, it)
+            np.testing.assert_array_equal(r.ehat, e)
+            _assert_post(algo, r.post, post)
+        else:
+            # BP: exact decisions except where a posterior sits within tolerance of 0
+            near0 = np.abs(post) <= BP_RTOL * np.maximum(1.0, np.abs(post).max(axis=1, keepdims=True))
+            same_it = r.iters == it
+            assert same_it.mean() > 0.99, f"iteration counts differ on {np.sum(~same_it)} shots"
+            rows = same_it
+            np.testing.assert_array_equal(r.ehat[rows][~near0[rows]], e[rows][~near0[rows]])
+            np.testing.assert_allclose(r.post[rows], post[rows], rtol=BP_RTOL, atol=1e-9)
+        if p is not None:
+            # property: a converged shot satisfies its syndrome
+            conv = r.converged
+            Hm = H.astype(np.int64)
+            assert np.all(((r.ehat[conv].astype(np.int64) @ Hm.T) % 2) == syn[conv])
+
+
+def test_full_size_headline_batch_properties(dec):
+    """BASELINE config at full size (2^20 shots/half would be the bench; here
+    2^18): every fixed-work random syndrome runs exactly 50 iterations, never
+    converges (rank(H)=232 < m=240 makes them unsatisfiable w.p. >= 255/256,
+    SURVEY.md §8d), a seeded sample matches the oracle bit for bit, and the
+    decode is deterministic run to run."""
+    import torch
+    from oracle import oracle
+    from qldpcsim_amd import codes
+    Hx, Hz = codes.load_code("LP118_0")
+    B = 1 << 18
+    g = torch.Generator(device="cuda").manual_seed(1)
+    syn = torch.randint(0, 2, (B, Hz.shape[0]), dtype=torch.uint8, device="cuda", generator=g)
+    r1 = dec.decode_batch(Hz, syn, 0.05 / 3, 50, algo="MS")
+    r2 = dec.decode_batch(Hz, syn, 0.05 / 3, 50, algo="MS")
+    torch.cuda.synchronize()
+    assert torch.equal(r1.ehat, r2.ehat) and torch.equal(r1.iters, r2.iters)
+    conv = ((r1.flags & 1) != 0)
+    it = r1.iters
+    # converged shots must satisfy the syndrome; all others ran max_iter
+    assert bool(torch.all(it[~conv] == 50))
+    assert conv.float().mean().item() < 0.02
+    idx = np.random.default_rng(3).choice(B, 256, replace=False)
+    sub = syn[torch.as_tensor(idx, device="cuda")].cpu().numpy()
+    e, its, _, _ = oracle.decode_batch("MS", Hz, sub, 0.05 / 3, 50, want_post=False)
+    np.testing.assert_array_equal(r1.ehat[torch.as_tensor(idx, device="cuda")].cpu().numpy(), e)
+    np.testing.assert_array_equal(it[torch.as_tensor(idx, device="cuda")].cpu().numpy(), its)
