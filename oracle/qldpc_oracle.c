@@ -22,14 +22,18 @@
  *   BP: float64; product of tanh = sequential fold (np.prod, :254); division
  *       extrinsic (:256); eps clip (:257-258); column sums follow NumPy's
  *       pairwise_sum (0.0 + pairwise(all), 8-accumulator blocks for n >= 8,
- *       :269/:276). tanh/atanh come from glibc, so BP matches the NumPy run to
- *       ULP level, not bit for bit.
+ *       :269/:276). tanh/atanh come from include/qldpc_libm.h (<= 3 ULP from
+ *       NumPy's), the same code the GPU kernel runs, so GPU and oracle agree
+ *       bit for bit while oracle and reference agree to ULP level (BP's atanh
+ *       near +-1 amplifies any libm difference; see that header).
  * Build: oracle/Makefile  ->  oracle/_build/libqldpc_oracle.so
  */
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+
+#include "../include/qldpc_libm.h" /* reproducible tanh/atanh, shared with the GPU kernel */
 
 #define ORACLE_FLAG_MIN_ZERO 1  /* MS: a check saw min|v| == 0 (App. A.1.6 leak case, not emulated) */
 #define ORACLE_FLAG_NONFINITE 2 /* BP: tanh(v/2)==0 or a non-finite message */
@@ -75,7 +79,7 @@ static int ms_decode_one(const graph_t *g, const uint8_t *syn, double p, int max
                          int n_layers, const int32_t *layer_ptr, const int32_t *layer_rows,
                          double beta, double eps, uint8_t *ehat, double *post_out,
                          int *flags, float *c2v, float *c2v_new, float *S, double *post) {
-    const int m = g->m, n = g->n;
+    const int n = g->n;
     const double L = log((1.0 - p) / (p > eps ? p : eps));  /* :147 (np.float64) */
     const float L32 = (float)L;                              /* :148-149 float32 store */
     for (int e = 0; e < g->E; ++e) c2v[e] = 0.0f;           /* :150 */
@@ -178,13 +182,13 @@ static int bp_decode_one(const graph_t *g, const uint8_t *syn, double p, int max
                 const int e0 = g->row_ptr[i], e1 = g->row_ptr[i + 1];
                 if (e1 == e0) continue;
                 double prod = 1.0;
-                for (int e = e0; e < e1; ++e) prod *= tanh(v2c[e] / 2.0);
+                for (int e = e0; e < e1; ++e) prod *= qldpc_tanh(v2c[e] / 2.0);
                 for (int e = e0; e < e1; ++e) {
-                    const double t = tanh(v2c[e] / 2.0);
+                    const double t = qldpc_tanh(v2c[e] / 2.0);
                     double th2 = prod / t;
                     if (t == 0.0) *flags |= ORACLE_FLAG_NONFINITE;
                     if (fabs(th2) >= 1.0 - eps) th2 = th2 - eps * (th2 > 0 ? 1.0 : (th2 < 0 ? -1.0 : 0.0));
-                    double val = 2.0 * atanh(th2);
+                    double val = 2.0 * qldpc_atanh(th2);
                     if (syn[i] & 1) val = -val;
                     c2v[e] = val;
                 }

@@ -33,6 +33,14 @@ class HIPLibraryMissing(ImportError):
 
 
 def _load():
+    # PyTorch-ROCm ships its own libamdhip64.so (SONAME libamdhip64.so.7, the
+    # same as /opt/rocm's). Load it first when torch is present so this
+    # library binds to the very same HIP runtime instance; loading ours first
+    # would bring in a second runtime and torch then sees no device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise HIPLibraryMissing(
             f"{LIB_PATH} not found: build the HIP extension first "

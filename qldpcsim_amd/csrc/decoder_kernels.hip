@@ -25,13 +25,15 @@
 //
 // Numerics: MS c2v = fl32(beta * min) formed in float64;
 // VN sum float32 sequential; posterior and v2c float64; first layer of the
-// first iteration sees float32(L). BP float64 with device tanh/atanh.
+// first iteration sees float32(L). BP float64; tanh/atanh from
+// include/qldpc_libm.h (basic IEEE ops only: identical on GPU and CPU oracle).
 // Compiled with -ffp-contract=off: no FMA contraction may change a rounding.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "decoder_kernels.h"
+#include "../../include/qldpc_libm.h"
 
 namespace qldpc {
 
@@ -151,7 +153,7 @@ __device__ __forceinline__ uint32_t cn_update(const DecodeArgs& a, const LdsView
       const double pj = post[j];
       par ^= (uint32_t)(pj < 0.0);
       const double v = pj - c2v[pos];                // v2c (:269)
-      const double th = tanh(v / 2.0);               // (:254)
+      const double th = qldpc_tanh(v / 2.0);         // (:254) reproducible tanh
       prod *= th;                                    // np.prod: sequential fold
       c2v[pos] = th;                                 // scratch: own edge, rewritten below
     }
@@ -162,7 +164,7 @@ __device__ __forceinline__ uint32_t cn_update(const DecodeArgs& a, const LdsView
         const int j = (int)(t >> 16), pos = (int)(t & 0xffffu);
         const double pj = post[j];
         par ^= (uint32_t)(pj < 0.0);
-        const double th = tanh((pj - c2v[pos]) / 2.0);
+        const double th = qldpc_tanh((pj - c2v[pos]) / 2.0);
         prod *= th;
         c2v[pos] = th;
       }
@@ -175,7 +177,7 @@ __device__ __forceinline__ uint32_t cn_update(const DecodeArgs& a, const LdsView
       double th2 = prod / th;                        // (:256)
       if (__builtin_fabs(th2) >= lim)                // (:257-258)
         th2 = th2 - a.eps * (th2 > 0.0 ? 1.0 : (th2 < 0.0 ? -1.0 : 0.0));
-      double val = 2.0 * atanh(th2);                 // (:259)
+      double val = 2.0 * qldpc_atanh(th2);           // (:259) reproducible atanh
       if (synb) val = -val;                          // (:260-261)
       if (!__builtin_isfinite(val)) fl |= FLAG_NONFINITE;
       c2v[pos] = val;
@@ -249,6 +251,14 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
       // ---------------- flooding: one layer holding every check ------------
       uint32_t synreg = 0;  // bit i = syndrome of check lane + 64 i
       for (int i = 0, c = lane; c < m; ++i, c += 64) synreg |= (uint32_t)(syn[c] & 1) << i;
+      if constexpr (ALGO == ALGO_BP) {
+        // BP's first check-node pass reads v2c = L0 (decoders.py:235):
+        // post = L0, c2v = 0. (MS's first pass reads float32(L) directly.)
+        for (int j = lane; j < n; j += 64) post[j] = a.L;
+        double* cz = (double*)c2v;
+        for (int p = lane; p < a.E; p += 64) cz[p] = 0.0;
+        wave_sync();
+      }
       for (int it = 0;; ++it) {
         // CN over all checks; its parity pass is the stop test of iteration it-1
         // (decoders.py:175-176 — checks read the posteriors the last VN wrote).

@@ -3,9 +3,10 @@ vectors and the pinned CPU oracle on identical syndromes.
 
 Bar:
   MS — hard decisions, iteration counts and float64 posteriors bit-exact.
-  BP — iteration counts and hard decisions exact; posteriors within
-       rtol 1e-5 (north-star tolerance; device tanh/atanh differ from
-       glibc/NumPy by ULPs).
+  BP — against the reference's golden vectors: iteration counts and hard
+       decisions exact, posteriors within rtol 1e-5 (north-star tolerance;
+       NumPy's tanh/arctanh vs include/qldpc_libm.h differ by <= 3 ULP);
+       against the CPU oracle (same libm code): bit-exact.
 """
 import numpy as np
 import pytest
@@ -103,6 +104,11 @@ def _channel(Hx, Hz, p, B, seed):
     ("LP118_0", "F", "BP", 0.05, 100, 512),
     ("LP118_0", "L", "BP", 0.05, 100, 256),
     ("bicycle", "F", "BP", 0.05, 30, 256),
+    ("LP118_0", "F", "BP", None, 5, 512),         # short horizon: every posterior within tolerance
+    ("LP118_0", "L", "BP", None, 3, 256),
+    ("LP118_0", "L", "MS", 0.05, 50, 2048),
+    ("LP118_0", "S", "MS", 0.05, 3, 256),
+    ("T", "F", "MS", 0.05, 50, 1024),
 ])
 def test_kernel_matches_oracle_batches(dec, code, sched, algo, p, max_iter, B):
     from oracle import oracle
@@ -121,18 +127,13 @@ def test_kernel_matches_oracle_batches(dec, code, sched, algo, p, max_iter, B):
         r = dec.decode_batch(H, syn, prior, max_iter, algo=algo, want_post=True,
                              layer_ptr=lp, layer_rows=lr)
         e, it, post, fl = oracle.decode_batch(algo, H, syn, prior, max_iter, lp, lr)
-        if algo == "MS":
-            np.testing.assert_array_equal(r.iters, it)
-            np.testing.assert_array_equal(r.ehat, e)
-            _assert_post(algo, r.post, post)
-        else:
-            # BP: exact decisions except where a posterior sits within tolerance of 0
-            near0 = np.abs(post) <= BP_RTOL * np.maximum(1.0, np.abs(post).max(axis=1, keepdims=True))
-            same_it = r.iters == it
-            assert same_it.mean() > 0.99, f"iteration counts differ on {np.sum(~same_it)} shots"
-            rows = same_it
-            np.testing.assert_array_equal(r.ehat[rows][~near0[rows]], e[rows][~near0[rows]])
-            np.testing.assert_allclose(r.post[rows], post[rows], rtol=BP_RTOL, atol=1e-9)
+        # MS and BP: bit-exact against the oracle on every shot (BP shares the
+        # reproducible tanh/atanh of include/qldpc_libm.h with the oracle; the
+        # oracle itself is pinned to the reference within 2.2e-8 relative).
+        np.testing.assert_array_equal(r.iters, it)
+        np.testing.assert_array_equal(r.ehat, e)
+        np.testing.assert_array_equal(r.post.view(np.uint64), post.view(np.uint64))
+        np.testing.assert_array_equal(r.flags & 6, np.where(fl != 0, r.flags & 6, 0))
         if p is not None:
             # property: a converged shot satisfies its syndrome
             conv = r.converged
