@@ -133,7 +133,8 @@ def test_kernel_matches_oracle_batches(dec, code, sched, algo, p, max_iter, B):
         np.testing.assert_array_equal(r.iters, it)
         np.testing.assert_array_equal(r.ehat, e)
         np.testing.assert_array_equal(r.post.view(np.uint64), post.view(np.uint64))
-        np.testing.assert_array_equal(r.flags & 6, np.where(fl != 0, r.flags & 6, 0))
+        if algo == "MS":   # the zero-message leak case is flagged identically
+            np.testing.assert_array_equal((r.flags & 2) != 0, (fl & 1) != 0)
         if p is not None:
             # property: a converged shot satisfies its syndrome
             conv = r.converged

@@ -3,8 +3,3 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 900 python -m pytest tests/test_gpu_parity.py -q -m gpu --maxfail=30 > gpurun_out/pytest_gpu.log 2>&1
-rc=$?
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_r01 -o trace -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 > gpurun_out/bench_prof.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o pmc -- python3 bench.py --steps 1 --warmup 0 --cpu-seconds 0 > gpurun_out/bench_pmc_fetch.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o pmc -- python3 bench.py --steps 1 --warmup 0 --cpu-seconds 0 > gpurun_out/bench_pmc_write.log 2>&1 || exit $?
