@@ -205,6 +205,12 @@ struct qldpc_schedule {
 
 static int align16(int x) { return (x + 15) & ~15; }
 
+// Uniform row degree 7 or 8 with LDS offsets that fit 16 bits -> the
+// unrolled kernel instantiation and its pre-scaled table format.
+static bool fast_table_ok(const qldpc_code* c) {
+  return (c->uniform_deg == 7 || c->uniform_deg == 8) && 8 * c->n < 65536 && 8 * c->E < 65536;
+}
+
 template <typename T>
 static int put(std::vector<uint8_t>& blob, const std::vector<T>& v) {
   const int off = align16((int)blob.size());
@@ -241,9 +247,20 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
   // One layer holding every row exactly once == flooding (decoders.py:122).
   s->layered = !(n_layers == 1 && (int)layers[0].size() == m);
 
-  std::vector<uint32_t> cn_tab(code->E);
-  for (int e = 0; e < code->E; ++e)
-    cn_tab[e] = ((uint32_t)code->vinv[code->col_idx[e]] << 16) | (uint32_t)code->edge_pos[e];
+  std::vector<uint32_t> cn_tab;
+  if (fast_table_ok(code)) {
+    // uniform row degree: rows padded to 8 entries, pre-scaled LDS byte offsets
+    // (4 * csc position) << 16 | (8 * relabeled variable)
+    cn_tab.assign((size_t)8 * m, 0);
+    for (int r = 0; r < m; ++r)
+      for (int e = code->row_ptr[r], k = 0; e < code->row_ptr[r + 1]; ++e, ++k)
+        cn_tab[(size_t)8 * r + k] = ((uint32_t)(4 * code->edge_pos[e]) << 16) |
+                                    (uint32_t)(8 * code->vinv[code->col_idx[e]]);
+  } else {
+    cn_tab.resize(code->E);
+    for (int e = 0; e < code->E; ++e)
+      cn_tab[e] = ((uint32_t)code->vinv[code->col_idx[e]] << 16) | (uint32_t)code->edge_pos[e];
+  }
   std::vector<uint16_t> row_ptr(code->row_ptr.begin(), code->row_ptr.end());
   std::vector<uint16_t> vn_ptr(code->csc_ptr.begin(), code->csc_ptr.end());
   s->off_cn_tab = put(s->blob, cn_tab);
@@ -329,7 +346,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
     return QLDPC_OK;
   }
   const qldpc_code* c = s->code;
-  const int dc = (c->uniform_deg == 7 || c->uniform_deg == 8) ? c->uniform_deg : 0;
+  const int dc = fast_table_ok(c) ? c->uniform_deg : 0;
   cfg.kernel = qldpc::select_kernel(algo, s->layered, dc);
   int off_c2v, off_synw, off_parw;
   wave_layout(c, s->layered, algo, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw);

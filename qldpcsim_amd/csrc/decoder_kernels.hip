@@ -87,8 +87,85 @@ struct LdsView {
   const uint16_t* adj_vars; // [*]
 };
 
+// Graph table entry formats (capi.cpp builds them):
+//  DC == 0 (generic):   cn_tab[row_ptr[c] + k] = (relabeled var << 16) | csc position
+//  DC  > 0 (uniform row degree DC, rows padded to 8 entries, 16-byte aligned):
+//                       cn_tab[8c + k] = (4 * csc position) << 16 | (8 * relabeled var)
+//                       i.e. ready-made LDS byte offsets into c2v (f32) and post (f64).
+template <int DC>
+__device__ __forceinline__ int tab_var(uint32_t t) { return DC ? (int)((t & 0xffffu) >> 3) : (int)(t >> 16); }
+template <int DC>
+__device__ __forceinline__ int tab_pos(uint32_t t) { return DC ? (int)(t >> 18) : (int)(t & 0xffffu); }
+
+__device__ __forceinline__ uint32_t hi_word(double d) { return (uint32_t)(__builtin_bit_cast(uint64_t, d) >> 32); }
+
 // ---------------------------------------------------------------------------
-// Check-node update of one check `c` (lane-local).
+// Min-sum check-node update for a uniform-degree code (DC = 7 or 8), the hot
+// loop of the headline workload (decoders.py:155-169 for one row):
+//   v_e   = post_j - c2v_e  (float64; FIRST: float32(L), :148-149)
+//   min1 / first argmin / min2 of |v_e|, sign product with the syndrome sign
+//   c2v_e = fl32(beta * (e == argmin ? min2 : min1)) with sign syn*prod*sign_e
+// Signs and the parity of the hard decisions are folded from the high words
+// (v_e is never -0.0 and post never -0.0 or NaN for finite L: DESIGN.md §4).
+// Returns the check's "unsatisfied" bit for the posteriors it read.
+// ---------------------------------------------------------------------------
+template <int DC, bool FIRST>
+__device__ __forceinline__ uint32_t cn_ms_uniform(const DecodeArgs& a, const uint32_t* tab,
+                                                  uint32_t synb, const unsigned char* post_b,
+                                                  unsigned char* c2v_b, int& fl) {
+  static_assert(DC >= 2 && DC <= 8, "uniform fast path handles row degrees 2..8");
+  const uint4 t0 = *(const uint4*)tab;
+  const uint4 t1 = *(const uint4*)(tab + 4);
+  const uint32_t t[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+  if constexpr (FIRST) {
+    // every v_e = float32(L): min1 = min2 = |L32|, argmin 0, sign_e = L32 < 0
+    const double vf = (double)a.L32;
+    const double av = __builtin_fabs(vf);
+    const float c = (float)(a.beta * av);
+    const uint32_t neg = (uint32_t)(vf < 0.0);
+    const uint32_t negprod = ((neg * DC) ^ synb) & 1u;
+    const float val = (neg ^ negprod) ? -c : c;
+    if (av == 0.0) fl |= FLAG_MIN_ZERO;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) *(float*)(c2v_b + (t[k] >> 16)) = val;
+    return 0;
+  } else {
+    double v[DC];
+    uint32_t ph = 0, sh = 0;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+      const double pj = *(const double*)(post_b + (t[k] & 0xffffu));
+      const float cv = *(const float*)(c2v_b + (t[k] >> 16));
+      v[k] = pj - (double)cv;                         // v2c = post - c2v (:177)
+      ph ^= hi_word(pj);                              // hard decision post < 0 (:174)
+      sh ^= hi_word(v[k]);                            // np.sign product (:157-159)
+    }
+    double min1 = __builtin_inf(), min2 = __builtin_inf();
+    int idx = 0;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+      const double av = __builtin_fabs(v[k]);
+      idx = (av < min1) ? k : idx;                    // first argmin (:161)
+      min2 = __builtin_fmin(min2, __builtin_fmax(min1, av));  // min of the rest (:162-164)
+      min1 = __builtin_fmin(min1, av);
+    }
+    if (__builtin_isinf(min1)) min1 = 0.0;            // (:165)
+    if (__builtin_isinf(min2)) min2 = 0.0;            // (:166)
+    if (min1 == 0.0) fl |= FLAG_MIN_ZERO;             // App. A.1.6 leak case (flagged)
+    const uint32_t negprod = ((sh >> 31) ^ synb) << 31;
+    const uint32_t c1 = __builtin_bit_cast(uint32_t, (float)(a.beta * min1));
+    const uint32_t c2 = __builtin_bit_cast(uint32_t, (float)(a.beta * min2));
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+      const uint32_t mag = (k == idx) ? c2 : c1;      // (:167-168)
+      *(uint32_t*)(c2v_b + (t[k] >> 16)) = mag | ((hi_word(v[k]) ^ negprod) & 0x80000000u);
+    }
+    return (ph >> 31) ^ synb;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Check-node update of one check `c` (lane-local), any degree.
 //   MS: decoders.py:155-169.  BP: decoders.py:249-262.
 // Returns the check's current parity XOR syndrome bit ("unsatisfied"),
 // computed from the hard decisions of the posteriors it reads (only
@@ -98,7 +175,12 @@ template <int ALGO, int DC>
 __device__ __forceinline__ uint32_t cn_update(const DecodeArgs& a, const LdsView& g, int c,
                                               uint32_t synb, bool first, const double* post,
                                               void* c2v_raw, int& fl) {
-  const int e0 = DC ? c * DC : (int)g.row_ptr[c];
+  if constexpr (ALGO == ALGO_MS && DC > 0) {
+    const uint32_t* tab = g.cn_tab + c * 8;
+    if (first) return cn_ms_uniform<DC, true>(a, tab, synb, (const unsigned char*)post, (unsigned char*)c2v_raw, fl);
+    return cn_ms_uniform<DC, false>(a, tab, synb, (const unsigned char*)post, (unsigned char*)c2v_raw, fl);
+  }
+  const int e0 = DC ? c * 8 : (int)g.row_ptr[c];
   const int deg = DC ? DC : (int)g.row_ptr[c + 1] - e0;
   uint32_t par = 0;
   if constexpr (ALGO == ALGO_MS) {
@@ -107,11 +189,9 @@ __device__ __forceinline__ uint32_t cn_update(const DecodeArgs& a, const LdsView
     int idx = 0;
     uint32_t negm = 0;
     const double vfirst = (double)a.L32;
-#pragma unroll
-    for (int k = 0; k < (DC ? DC : 32); ++k) {
-      if (!DC && k >= deg) break;
+    for (int k = 0; k < deg; ++k) {
       const uint32_t t = g.cn_tab[e0 + k];
-      const int j = (int)(t >> 16), pos = (int)(t & 0xffffu);
+      const int j = tab_var<DC>(t), pos = tab_pos<DC>(t);
       double v;
       if (first) {
         v = vfirst;                                   // float32(L) (:148-149)
@@ -134,10 +214,8 @@ __device__ __forceinline__ uint32_t cn_update(const DecodeArgs& a, const LdsView
     // c2v_e = fl32(beta * syn * prod * min_e / sign_e): magnitude rounded from
     // the float64 product once, sign = syn * prod * sign_e (:167-168).
     const float c1 = (float)(a.beta * min1), c2 = (float)(a.beta * min2);
-#pragma unroll
-    for (int k = 0; k < (DC ? DC : 32); ++k) {
-      if (!DC && k >= deg) break;
-      const int pos = (int)(g.cn_tab[e0 + k] & 0xffffu);
+    for (int k = 0; k < deg; ++k) {
+      const int pos = tab_pos<DC>(g.cn_tab[e0 + k]);
       const float mag = (k == idx) ? c2 : c1;
       c2v[pos] = (((negm >> k) & 1u) ^ negprod) ? -mag : mag;
     }
@@ -149,7 +227,7 @@ __device__ __forceinline__ uint32_t cn_update(const DecodeArgs& a, const LdsView
     for (int k = 0; k < (DC ? DC : 32); ++k) {
       if (!DC && k >= deg) break;
       const uint32_t t = g.cn_tab[e0 + k];
-      const int j = (int)(t >> 16), pos = (int)(t & 0xffffu);
+      const int j = tab_var<DC>(t), pos = tab_pos<DC>(t);
       const double pj = post[j];
       par ^= (uint32_t)(pj < 0.0);
       const double v = pj - c2v[pos];                // v2c (:269)
@@ -161,7 +239,7 @@ __device__ __forceinline__ uint32_t cn_update(const DecodeArgs& a, const LdsView
       // generic degrees > 32: second half of the fold (rare; bicycle = 18)
       for (int k = 32; k < deg; ++k) {
         const uint32_t t = g.cn_tab[e0 + k];
-        const int j = (int)(t >> 16), pos = (int)(t & 0xffffu);
+        const int j = tab_var<DC>(t), pos = tab_pos<DC>(t);
         const double pj = post[j];
         par ^= (uint32_t)(pj < 0.0);
         const double th = qldpc_tanh((pj - c2v[pos]) / 2.0);
@@ -171,7 +249,7 @@ __device__ __forceinline__ uint32_t cn_update(const DecodeArgs& a, const LdsView
     }
     const double lim = 1.0 - a.eps;
     for (int k = 0; k < deg; ++k) {
-      const int pos = (int)(g.cn_tab[e0 + k] & 0xffffu);
+      const int pos = tab_pos<DC>(g.cn_tab[e0 + k]);
       const double th = c2v[pos];
       if (th == 0.0) fl |= FLAG_NONFINITE;
       double th2 = prod / th;                        // (:256)
@@ -263,8 +341,13 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
         // CN over all checks; its parity pass is the stop test of iteration it-1
         // (decoders.py:175-176 — checks read the posteriors the last VN wrote).
         uint32_t unsat = 0;
-        for (int i = 0, c = lane; c < m; ++i, c += 64)
-          unsat |= cn_update<ALGO, DC>(a, g, c, (synreg >> i) & 1u, it == 0, post, c2v, fl);
+        if (it == 0) {
+          for (int i = 0, c = lane; c < m; ++i, c += 64)
+            (void)cn_update<ALGO, DC>(a, g, c, (synreg >> i) & 1u, true, post, c2v, fl);
+        } else {
+          for (int i = 0, c = lane; c < m; ++i, c += 64)
+            unsat |= cn_update<ALGO, DC>(a, g, c, (synreg >> i) & 1u, false, post, c2v, fl);
+        }
         if (it > 0 && ballot(unsat != 0) == 0) {
           iters = it;
           conv = true;
@@ -278,10 +361,10 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
           // both branches of the reference return max_iter, :176 / :182)
           uint32_t un = 0;
           for (int i = 0, c = lane; c < m; ++i, c += 64) {
-            const int e0 = DC ? c * DC : (int)g.row_ptr[c];
+            const int e0 = DC ? c * 8 : (int)g.row_ptr[c];
             const int deg = DC ? DC : (int)g.row_ptr[c + 1] - e0;
             uint32_t par = 0;
-            for (int k = 0; k < deg; ++k) par ^= (uint32_t)(post[g.cn_tab[e0 + k] >> 16] < 0.0);
+            for (int k = 0; k < deg; ++k) par ^= (uint32_t)(post[tab_var<DC>(g.cn_tab[e0 + k])] < 0.0);
             un |= par ^ ((synreg >> i) & 1u);
           }
           conv = ballot(un != 0) == 0;
