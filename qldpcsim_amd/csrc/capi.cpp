@@ -197,7 +197,7 @@ struct qldpc_schedule {
   int n_layers = 0;
   std::vector<uint8_t> blob;  // LDS image of the graph tables
   int off_cn_tab = 0, off_row_ptr = 0, off_vn_ptr = 0, off_vn_chk = 0;
-  int off_lay_ptr = 0, off_lay_rows = 0, off_adj_ptr = 0, off_adj_vars = 0;
+  int off_lay_ptr = 0, off_lay_rows = 0, off_adj_ptr = 0, off_adj_vars = 0, off_chunk_dmax = 0;
   unsigned char* d_blob = nullptr;
   LaunchCfg cfg[2];           // per algo
   std::mutex mu;
@@ -262,10 +262,16 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
       cn_tab[e] = ((uint32_t)code->vinv[code->col_idx[e]] << 16) | (uint32_t)code->edge_pos[e];
   }
   std::vector<uint16_t> row_ptr(code->row_ptr.begin(), code->row_ptr.end());
-  std::vector<uint16_t> vn_ptr(code->csc_ptr.begin(), code->csc_ptr.end());
+  std::vector<uint32_t> vn_ptr(n);  // csc start | degree << 16
+  for (int j = 0; j < n; ++j)
+    vn_ptr[j] = (uint32_t)code->csc_ptr[j] | ((uint32_t)(code->csc_ptr[j + 1] - code->csc_ptr[j]) << 16);
   s->off_cn_tab = put(s->blob, cn_tab);
   s->off_row_ptr = put(s->blob, row_ptr);
   s->off_vn_ptr = put(s->blob, vn_ptr);
+  std::vector<uint8_t> chunk_dmax((n + 63) / 64, 0);   // VN passes unroll to this (<= 255)
+  for (int j = 0; j < n; ++j)
+    chunk_dmax[j >> 6] = (uint8_t)std::min(255, std::max<int>(chunk_dmax[j >> 6], code->csc_ptr[j + 1] - code->csc_ptr[j]));
+  s->off_chunk_dmax = put(s->blob, chunk_dmax);
   if (s->layered) {
     std::vector<uint16_t> vn_chk(code->E), lay_ptr(n_layers + 1, 0), lay_rows, adj_ptr(n_layers + 1, 0), adj_vars;
     for (int p = 0; p < code->E; ++p) {
@@ -329,7 +335,7 @@ static void wave_layout(const qldpc_code* c, bool layered, int algo, int* bytes,
                         int* off_synw, int* off_parw) {
   int off = align16(8 * c->n);
   *off_c2v = off;
-  off = align16(off + (algo == QLDPC_ALGO_MS ? 4 : 8) * c->E);
+  off = align16(off + (algo == QLDPC_ALGO_MS ? 4 : 8) * (c->E + 8));  // +8: VN over-read pad
   const int words = 2 * ((c->m + 63) / 64);
   *off_synw = off;
   if (layered) off = align16(off + 4 * words);
@@ -356,7 +362,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   HIP_TRY(qldpc::configure_kernel(cfg.kernel, max_lds));
   const int blob = (int)s->blob.size();
   int best_waves = 0;
-  for (int w = 16; w >= 1; --w) {
+  for (int w = QLDPC_MAX_THREADS / 64; w >= 1; --w) {
     const int lds = blob + w * cfg.wave_bytes;
     if (lds > max_lds) continue;
     int nb = 0;
@@ -459,6 +465,7 @@ extern "C" int qldpc_decode_device(const qldpc_code* code, const qldpc_schedule*
   a.off_lay_rows = sched->off_lay_rows;
   a.off_adj_ptr = sched->off_adj_ptr;
   a.off_adj_vars = sched->off_adj_vars;
+  a.off_chunk_dmax = sched->off_chunk_dmax;
   wave_layout(code, sched->layered, algo, &a.wave_bytes, &a.off_c2v, &a.off_synw, &a.off_parw);
   a.m = code->m;
   a.n = code->n;
@@ -514,6 +521,7 @@ extern "C" int qldpc_decode_host(const qldpc_code* code_c, const qldpc_schedule*
   if (batch < 0) return fail(QLDPC_EINVAL, "negative batch");
   if (batch == 0) return QLDPC_OK;
   if (!h_syn || !h_ehat || !h_iters) return fail(QLDPC_EINVAL, "null host buffer");
+  if (code->device < 0) return fail(QLDPC_EHIP, "no HIP device was visible when the code was created");
   std::lock_guard<std::mutex> lk(code->ws_mu);
   const int m = code->m, n = code->n;
   if (batch > code->ws_cap) {

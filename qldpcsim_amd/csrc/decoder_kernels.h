@@ -3,6 +3,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// threads per workgroup the kernels are compiled for (waves per WG <= this/64)
+#define QLDPC_MAX_THREADS 768
+
 namespace qldpc {
 
 enum { ALGO_MS = 0, ALGO_BP = 1 };
@@ -14,7 +17,7 @@ struct DecodeArgs {
   const unsigned char* blob;  // device copy of the LDS table image
   int blob_bytes;             // multiple of 16
   int off_cn_tab, off_row_ptr, off_vn_ptr, off_vn_chk;
-  int off_lay_ptr, off_lay_rows, off_adj_ptr, off_adj_vars;
+  int off_lay_ptr, off_lay_rows, off_adj_ptr, off_adj_vars, off_chunk_dmax;
   int wave_bytes;             // per-wave state slice (multiple of 16)
   int off_c2v, off_synw, off_parw;  // inside a wave slice (post f64[n] at 0)
   int m, n, E, n_layers;

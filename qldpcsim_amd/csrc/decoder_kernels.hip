@@ -35,6 +35,10 @@
 #include "decoder_kernels.h"
 #include "../../include/qldpc_libm.h"
 
+#ifndef QLDPC_ABLATE
+#define QLDPC_ABLATE 0  // timing-only builds: 1 = skip VN, 2 = skip CN (flooding)
+#endif
+
 namespace qldpc {
 
 __device__ __forceinline__ void wave_sync() {
@@ -79,7 +83,8 @@ __device__ __forceinline__ void store_bits64(uint32_t* words, int c0, int pred, 
 struct LdsView {
   const uint32_t* cn_tab;   // [E] (relabeled var << 16) | csc position, CSR edge order
   const uint16_t* row_ptr;  // [m+1]
-  const uint16_t* vn_ptr;   // [n+1]
+  const uint32_t* vn_info;  // [n]   csc start | degree << 16
+  const uint8_t* chunk_dmax; // [ceil(n/64)] max degree of relabeled variables 64c..64c+63
   const uint16_t* vn_chk;   // [E]   check of each CSC position (layered)
   const uint16_t* lay_ptr;  // [L+1]
   const uint16_t* lay_rows; // [*]
@@ -109,58 +114,83 @@ __device__ __forceinline__ uint32_t hi_word(double d) { return (uint32_t)(__buil
 // (v_e is never -0.0 and post never -0.0 or NaN for finite L: DESIGN.md §4).
 // Returns the check's "unsatisfied" bit for the posteriors it read.
 // ---------------------------------------------------------------------------
-template <int DC, bool FIRST>
-__device__ __forceinline__ uint32_t cn_ms_uniform(const DecodeArgs& a, const uint32_t* tab,
-                                                  uint32_t synb, const unsigned char* post_b,
+template <int DC, bool FIRST, int NC>
+__device__ __forceinline__ uint32_t cn_ms_uniform(const DecodeArgs& a, const uint32_t* const* tabs,
+                                                  const uint32_t* synb, const bool* live,
+                                                  const unsigned char* post_b,
                                                   unsigned char* c2v_b, int& fl) {
+  // NC independent checks per call: every LDS read of all NC checks is issued
+  // before any arithmetic, so a wave keeps 2*DC*NC reads in flight.
   static_assert(DC >= 2 && DC <= 8, "uniform fast path handles row degrees 2..8");
-  const uint4 t0 = *(const uint4*)tab;
-  const uint4 t1 = *(const uint4*)(tab + 4);
-  const uint32_t t[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+  uint32_t t[NC][8];
+#pragma unroll
+  for (int q = 0; q < NC; ++q) {
+    const uint4 t0 = *(const uint4*)tabs[q];
+    const uint4 t1 = *(const uint4*)(tabs[q] + 4);
+    t[q][0] = t0.x; t[q][1] = t0.y; t[q][2] = t0.z; t[q][3] = t0.w;
+    t[q][4] = t1.x; t[q][5] = t1.y; t[q][6] = t1.z; t[q][7] = t1.w;
+  }
   if constexpr (FIRST) {
     // every v_e = float32(L): min1 = min2 = |L32|, argmin 0, sign_e = L32 < 0
     const double vf = (double)a.L32;
     const double av = __builtin_fabs(vf);
     const float c = (float)(a.beta * av);
     const uint32_t neg = (uint32_t)(vf < 0.0);
-    const uint32_t negprod = ((neg * DC) ^ synb) & 1u;
-    const float val = (neg ^ negprod) ? -c : c;
     if (av == 0.0) fl |= FLAG_MIN_ZERO;
 #pragma unroll
-    for (int k = 0; k < DC; ++k) *(float*)(c2v_b + (t[k] >> 16)) = val;
+    for (int q = 0; q < NC; ++q) {
+      const uint32_t negprod = ((neg * DC) ^ synb[q]) & 1u;
+      const float val = (neg ^ negprod) ? -c : c;
+      if (live[q]) {
+#pragma unroll
+        for (int k = 0; k < DC; ++k) *(float*)(c2v_b + (t[q][k] >> 16)) = val;
+      }
+    }
     return 0;
   } else {
-    double v[DC];
-    uint32_t ph = 0, sh = 0;
+    double v[NC][DC];
+    uint32_t ph[NC], sh[NC];
 #pragma unroll
-    for (int k = 0; k < DC; ++k) {
-      const double pj = *(const double*)(post_b + (t[k] & 0xffffu));
-      const float cv = *(const float*)(c2v_b + (t[k] >> 16));
-      v[k] = pj - (double)cv;                         // v2c = post - c2v (:177)
-      ph ^= hi_word(pj);                              // hard decision post < 0 (:174)
-      sh ^= hi_word(v[k]);                            // np.sign product (:157-159)
-    }
-    double min1 = __builtin_inf(), min2 = __builtin_inf();
-    int idx = 0;
+    for (int q = 0; q < NC; ++q) {
+      ph[q] = 0;
+      sh[q] = 0;
 #pragma unroll
-    for (int k = 0; k < DC; ++k) {
-      const double av = __builtin_fabs(v[k]);
-      idx = (av < min1) ? k : idx;                    // first argmin (:161)
-      min2 = __builtin_fmin(min2, __builtin_fmax(min1, av));  // min of the rest (:162-164)
-      min1 = __builtin_fmin(min1, av);
+      for (int k = 0; k < DC; ++k) {
+        const double pj = *(const double*)(post_b + (t[q][k] & 0xffffu));
+        const float cv = *(const float*)(c2v_b + (t[q][k] >> 16));
+        v[q][k] = pj - (double)cv;                    // v2c = post - c2v (:177)
+        ph[q] ^= hi_word(pj);                         // hard decision post < 0 (:174)
+        sh[q] ^= hi_word(v[q][k]);                    // np.sign product (:157-159)
+      }
     }
-    if (__builtin_isinf(min1)) min1 = 0.0;            // (:165)
-    if (__builtin_isinf(min2)) min2 = 0.0;            // (:166)
-    if (min1 == 0.0) fl |= FLAG_MIN_ZERO;             // App. A.1.6 leak case (flagged)
-    const uint32_t negprod = ((sh >> 31) ^ synb) << 31;
-    const uint32_t c1 = __builtin_bit_cast(uint32_t, (float)(a.beta * min1));
-    const uint32_t c2 = __builtin_bit_cast(uint32_t, (float)(a.beta * min2));
+    uint32_t unsat = 0;
 #pragma unroll
-    for (int k = 0; k < DC; ++k) {
-      const uint32_t mag = (k == idx) ? c2 : c1;      // (:167-168)
-      *(uint32_t*)(c2v_b + (t[k] >> 16)) = mag | ((hi_word(v[k]) ^ negprod) & 0x80000000u);
+    for (int q = 0; q < NC; ++q) {
+      double min1 = __builtin_inf(), min2 = __builtin_inf();
+      int idx = 0;
+#pragma unroll
+      for (int k = 0; k < DC; ++k) {
+        const double av = __builtin_fabs(v[q][k]);
+        idx = (av < min1) ? k : idx;                  // first argmin (:161)
+        min2 = __builtin_fmin(min2, __builtin_fmax(min1, av));  // min of the rest (:162-164)
+        min1 = __builtin_fmin(min1, av);
+      }
+      if (__builtin_isinf(min1)) min1 = 0.0;          // (:165)
+      if (__builtin_isinf(min2)) min2 = 0.0;          // (:166)
+      if (min1 == 0.0 && live[q]) fl |= FLAG_MIN_ZERO;  // App. A.1.6 leak case (flagged)
+      const uint32_t negprod = ((sh[q] >> 31) ^ synb[q]) << 31;
+      const uint32_t c1 = __builtin_bit_cast(uint32_t, (float)(a.beta * min1));
+      const uint32_t c2 = __builtin_bit_cast(uint32_t, (float)(a.beta * min2));
+      if (live[q]) {
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+          const uint32_t mag = (k == idx) ? c2 : c1;  // (:167-168)
+          *(uint32_t*)(c2v_b + (t[q][k] >> 16)) = mag | ((hi_word(v[q][k]) ^ negprod) & 0x80000000u);
+        }
+        unsat |= (ph[q] >> 31) ^ synb[q];
+      }
     }
-    return (ph >> 31) ^ synb;
+    return unsat;
   }
 }
 
@@ -176,9 +206,11 @@ __device__ __forceinline__ uint32_t cn_update(const DecodeArgs& a, const LdsView
                                               uint32_t synb, bool first, const double* post,
                                               void* c2v_raw, int& fl) {
   if constexpr (ALGO == ALGO_MS && DC > 0) {
-    const uint32_t* tab = g.cn_tab + c * 8;
-    if (first) return cn_ms_uniform<DC, true>(a, tab, synb, (const unsigned char*)post, (unsigned char*)c2v_raw, fl);
-    return cn_ms_uniform<DC, false>(a, tab, synb, (const unsigned char*)post, (unsigned char*)c2v_raw, fl);
+    const uint32_t* tabs[1] = {g.cn_tab + c * 8};
+    const uint32_t sb[1] = {synb};
+    const bool live[1] = {true};
+    if (first) return cn_ms_uniform<DC, true, 1>(a, tabs, sb, live, (const unsigned char*)post, (unsigned char*)c2v_raw, fl);
+    return cn_ms_uniform<DC, false, 1>(a, tabs, sb, live, (const unsigned char*)post, (unsigned char*)c2v_raw, fl);
   }
   const int e0 = DC ? c * 8 : (int)g.row_ptr[c];
   const int deg = DC ? DC : (int)g.row_ptr[c + 1] - e0;
@@ -267,24 +299,56 @@ __device__ __forceinline__ uint32_t cn_update(const DecodeArgs& a, const LdsView
 // Variable-node update of relabeled variable j: column sum in ascending check
 // order. MS: float32 sequential (np.sum axis=0, decoders.py:172), post = L +
 // (f64)S (:173). BP: np.sum pairwise rule, post = L0 + S (:269, :276).
+// vn_info[j] = csc start | degree << 16.
+template <int K>
+__device__ __forceinline__ float ms_colsum(const float* c, int d) {
+  // K unconditional loads (the c2v region is padded by 8 floats, so reading
+  // past a short column stays inside this wave's slice), then the sequential
+  // sum with the missing terms replaced by +0.0f — exact, since the running
+  // sum starts at +0.0f and is never -0.0f.
+  float x[K];
+#pragma unroll
+  for (int t = 0; t < K; ++t) x[t] = c[t];
+  float s = 0.0f;
+#pragma unroll
+  for (int t = 0; t < K; ++t) s += (t < d) ? x[t] : 0.0f;
+  return s;
+}
+
+// dmax: wave-uniform upper bound of the degrees of the variables this pass
+// covers (per 64-variable chunk, from the host), so the loads are unrolled.
 template <int ALGO>
 __device__ __forceinline__ double vn_post(const DecodeArgs& a, const LdsView& g, int j,
-                                          const void* c2v_raw) {
-  const int p0 = g.vn_ptr[j], p1 = g.vn_ptr[j + 1];
+                                          const void* c2v_raw, int dmax) {
+  const uint32_t info = g.vn_info[j];
+  const int p0 = (int)(info & 0xffffu), d = (int)(info >> 16);
   if constexpr (ALGO == ALGO_MS) {
-    const float* c2v = (const float*)c2v_raw;
-    float s = 0.0f;
-    for (int p = p0; p < p1; ++p) s += c2v[p];
+    const float* c = (const float*)c2v_raw + p0;
+    float s;
+    switch (dmax) {
+      case 0: s = 0.0f; break;
+      case 1: s = ms_colsum<1>(c, d); break;
+      case 2: s = ms_colsum<2>(c, d); break;
+      case 3: s = ms_colsum<3>(c, d); break;
+      case 4: s = ms_colsum<4>(c, d); break;
+      case 5: s = ms_colsum<5>(c, d); break;
+      case 6: s = ms_colsum<6>(c, d); break;
+      case 7: s = ms_colsum<7>(c, d); break;
+      case 8: s = ms_colsum<8>(c, d); break;
+      default:
+        s = 0.0f;
+        for (int t = 0; t < d; ++t) s += c[t];
+    }
     return a.L + (double)s;
   } else {
     const double* c2v = (const double*)c2v_raw;
-    if (p1 == p0) return a.L;                        // L_post[j] = L0 (:277-278)
-    return a.L + np_pairwise_sum(c2v + p0, p1 - p0);
+    if (d == 0) return a.L;                          // L_post[j] = L0 (:277-278)
+    return a.L + np_pairwise_sum(c2v + p0, d);
   }
 }
 
 template <int ALGO, bool LAYERED, int DC>
-__global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
+__global__ void __launch_bounds__(QLDPC_MAX_THREADS) decode_kernel(DecodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
 
   // Stage the read-only graph blob into LDS (16-byte vector copies).
@@ -299,7 +363,8 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
   LdsView g;
   g.cn_tab = (const uint32_t*)(lds + a.off_cn_tab);
   g.row_ptr = (const uint16_t*)(lds + a.off_row_ptr);
-  g.vn_ptr = (const uint16_t*)(lds + a.off_vn_ptr);
+  g.vn_info = (const uint32_t*)(lds + a.off_vn_ptr);
+  g.chunk_dmax = (const uint8_t*)(lds + a.off_chunk_dmax);
   g.vn_chk = (const uint16_t*)(lds + a.off_vn_chk);
   g.lay_ptr = (const uint16_t*)(lds + a.off_lay_ptr);
   g.lay_rows = (const uint16_t*)(lds + a.off_lay_rows);
@@ -341,7 +406,21 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
         // CN over all checks; its parity pass is the stop test of iteration it-1
         // (decoders.py:175-176 — checks read the posteriors the last VN wrote).
         uint32_t unsat = 0;
-        if (it == 0) {
+        if constexpr (QLDPC_ABLATE == 2) {
+          unsat = 1;
+        } else if constexpr (ALGO == ALGO_MS && DC > 0) {
+          // two checks (c, c + 64) per lane per step; a missing second check
+          // re-reads check c's row (in bounds) and skips its stores
+          for (int i = 0, c = lane; c < m; ++i, c += 64) {
+            const uint32_t* tabs[1] = {g.cn_tab + c * 8};
+            const uint32_t sb[1] = {(synreg >> i) & 1u};
+            const bool live[1] = {true};
+            if (it == 0)
+              (void)cn_ms_uniform<DC, true, 1>(a, tabs, sb, live, (const unsigned char*)post, (unsigned char*)c2v, fl);
+            else
+              unsat |= cn_ms_uniform<DC, false, 1>(a, tabs, sb, live, (const unsigned char*)post, (unsigned char*)c2v, fl);
+          }
+        } else if (it == 0) {
           for (int i = 0, c = lane; c < m; ++i, c += 64)
             (void)cn_update<ALGO, DC>(a, g, c, (synreg >> i) & 1u, true, post, c2v, fl);
         } else {
@@ -354,7 +433,13 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
           break;
         }
         wave_sync();
-        for (int j = lane; j < n; j += 64) post[j] = vn_post<ALGO>(a, g, j, c2v);
+        if constexpr (QLDPC_ABLATE != 1) {
+          for (int j0 = 0; j0 < n; j0 += 64) {
+            const int dmax = __builtin_amdgcn_readfirstlane((int)g.chunk_dmax[j0 >> 6]);
+            const int j = j0 + lane;
+            if (j < n) post[j] = vn_post<ALGO>(a, g, j, c2v, dmax);
+          }
+        }
         wave_sync();
         if (it + 1 == a.max_iter) {
           // final stop test after the last VN (its result only sets the flag:
@@ -412,10 +497,11 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
           for (int q = v0 + lane; q < v1; q += 64) {
             const int j = g.adj_vars[q];
             const double old = post[j];
-            const double nw = vn_post<ALGO>(a, g, j, c2v);
+            const double nw = vn_post<ALGO>(a, g, j, c2v, -1);
             post[j] = nw;
             if ((old < 0.0) != (nw < 0.0)) {
-              for (int p = g.vn_ptr[j]; p < g.vn_ptr[j + 1]; ++p) {
+              const uint32_t info = g.vn_info[j];
+              for (int p = (int)(info & 0xffffu), pe = p + (int)(info >> 16); p < pe; ++p) {
                 const int c = g.vn_chk[p];
                 atomicXor(&parw[c >> 5], 1u << (c & 31));
               }

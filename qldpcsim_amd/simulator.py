@@ -145,8 +145,9 @@ def simulate_p(Hx: np.ndarray, Hz: np.ndarray, p: float, shots: int = 1000, decT
     lpX, lrX = pack_layers(layersX, Hz.shape[0])    # X half decodes Hz with Hx's layers
     lpZ, lrZ = pack_layers(layersZ, Hx.shape[0])    # Z half decodes Hx with Hz's layers
 
-    # this rank's share of the shots
+    # this rank's contiguous share of the shots
     my_shots = shots // world + (1 if rank < shots % world else 0)
+    my_start = rank * (shots // world) + min(rank, shots % world)
     seed = None if rngSeed is None else [int(rngSeed), int(rank)]
     rng = np.random.default_rng(seed)
     tot = {k: 0 for k in COUNTER_KEYS}
@@ -155,7 +156,7 @@ def simulate_p(Hx: np.ndarray, Hz: np.ndarray, p: float, shots: int = 1000, decT
     while done < my_shots:
         B = min(batch_size, my_shots - done)
         if samples is not None:
-            sl = slice(done, done + B)
+            sl = slice(my_start + done, my_start + done + B)
             sy_z, sy_x, errX, errZ = (np.asarray(a)[sl].astype(np.uint8) for a in samples)
         else:
             sy_z, sy_x, errX, errZ = sample_channel(Hx, Hz, p, B, rng)

@@ -1,0 +1,119 @@
+"""Host logic of the drop-in simulator: matrix loading, layer construction and
+cross-wiring, outcome counting, the channel sampler and the results table."""
+import numpy as np
+import pytest
+
+from qldpcsim_amd import codes, schedule
+from qldpcsim_amd.simulator import count_outcomes, format_results, load_matrix, sample_channel
+
+
+def _layerize_literal(H, serial=False):
+    # simulator.py:212-224, restated independently
+    out, m, up, dn = [], H.shape[0], 1, 0
+    while up <= m:
+        if H[dn:up].sum(axis=0).max() > 1 or (serial and up > dn + 1):
+            out.append(list(range(dn, up - 1)))
+            dn = up - 1
+        else:
+            up += 1
+    out.append(list(range(dn, up - 1)))
+    return out
+
+
+@pytest.mark.parametrize("name,nx,nz", [("LP118_0", 13, 11), ("LP118_2", 13, 11), ("LP04_0", 10, 9)])
+def test_layer_counts_match_survey(name, nx, nz):
+    Hx, Hz = codes.load_code(name)
+    lx, lz = schedule.select_layers(Hx, Hz, "L")
+    assert (len(lx), len(lz)) == (nx, nz)
+    for H, ls in ((Hx, lx), (Hz, lz)):
+        assert [list(l) for l in ls] == _layerize_literal(H)
+        for l in ls:                                    # column-disjoint on the matrix they came from
+            assert H[l].sum(axis=0).max() <= 1
+
+
+def test_serial_and_flooding_layers():
+    Hx, Hz = codes.load_code("LP04_0")
+    sx, sz = schedule.select_layers(Hx, Hz, "S")
+    assert [list(l) for l in sx] == [[i] for i in range(Hx.shape[0])]
+    fx, fz = schedule.select_layers(Hx, Hz, "F")
+    assert len(fx) == 1 and list(fx[0]) == list(range(Hx.shape[0]))
+    with pytest.raises(ValueError, match="Unrecognized decoder scheduling option"):
+        schedule.select_layers(Hx, Hz, "Q")
+
+
+def test_pack_layers():
+    ptr, rows = schedule.pack_layers([np.array([0, 2]), np.array([1])], 3)
+    assert ptr.tolist() == [0, 2, 3] and rows.tolist() == [0, 2, 1]
+    with pytest.raises(IndexError):
+        schedule.pack_layers([np.array([5])], 3)
+    p2, r2 = schedule.pack_layers(None, 4)
+    assert p2.tolist() == [0, 4] and r2.tolist() == [0, 1, 2, 3]
+
+
+def test_load_matrix_npy_and_text(tmp_path):
+    M = np.array([[1, 0, 3], [2, 1, 1]])
+    np.save(tmp_path / "m.npy", M)
+    (tmp_path / "m.txt").write_text("1 0 3\n\n2 1 1\n")
+    for p in ("m.npy", "m.txt"):
+        L = load_matrix(str(tmp_path / p))
+        assert L.dtype == np.int8
+        np.testing.assert_array_equal(L, M % 2)
+
+
+def _count_literal(Hx, Hz, sy_z, sy_x, errX, errZ, eX, eZ, itX, itZ):
+    # simulator.py:291-303, one shot at a time
+    c = dict(DecFailures_X=0, DecFailures_Z=0, decSuccessExact=0, decSuccessDegen=0,
+             nIterAccX=0, nIterAccZ=0)
+    for k in range(len(itX)):
+        c["nIterAccX"] += int(itX[k])
+        c["nIterAccZ"] += int(itZ[k])
+        ex, ez = errX[k].astype(int), errZ[k].astype(int)
+        dx, dz = eX[k].astype(np.int8), eZ[k].astype(np.int8)
+        if np.array_equal(ex, dx) and np.array_equal(ez, dz):
+            c["decSuccessExact"] += 1
+        elif ((Hz @ (ex ^ dx)) == 0).all() and ((Hx @ (ez ^ dz)) == 0).all():
+            c["decSuccessDegen"] += 1
+        if not np.array_equal(sy_z[k].astype(int), (Hz.dot(dx)) % 2):
+            c["DecFailures_X"] += 1
+        if not np.array_equal(sy_x[k].astype(int), (Hx.dot(dz)) % 2):
+            c["DecFailures_Z"] += 1
+    return c
+
+
+def test_count_outcomes_matches_per_shot_restatement():
+    rng = np.random.default_rng(3)
+    Hx, Hz = codes.load_code("LP04_0")
+    B = 300
+    sy_z, sy_x, errX, errZ = sample_channel(Hx, Hz, 0.08, B, rng)
+    # estimates: exact for some shots, syndrome-equivalent for others, wrong for the rest
+    eX, eZ = errX.copy(), errZ.copy()
+    flip = rng.random(B) < 0.3
+    eX[flip, rng.integers(0, Hx.shape[1], flip.sum())] ^= 1
+    eZ[rng.random(B) < 0.2, 0] ^= 1
+    Hs = Hx.astype(np.int64)                      # a stabilizer of the X-check space
+    sel = rng.random(B) < 0.1
+    eZ[sel] ^= Hs[0].astype(np.uint8)
+    itX = rng.integers(1, 50, B)
+    itZ = rng.integers(1, 50, B)
+    got = count_outcomes(Hx, Hz, sy_z, sy_x, errX, errZ, eX, eZ, itX, itZ)
+    assert got == _count_literal(Hx, Hz, sy_z, sy_x, errX, errZ, eX, eZ, itX, itZ)
+
+
+def test_channel_sampler_statistics_and_syndromes():
+    rng = np.random.default_rng(11)
+    Hx, Hz = codes.load_code("LP118_0")
+    p = 0.06
+    sy_z, sy_x, errX, errZ = sample_channel(Hx, Hz, p, 20000, rng)
+    # X flip marginal = P(X)+P(Y) = 2p/3
+    assert abs(errX.mean() - 2 * p / 3) < 0.002 and abs(errZ.mean() - 2 * p / 3) < 0.002
+    assert abs((errX & errZ).mean() - p / 3) < 0.002             # Y errors
+    np.testing.assert_array_equal(sy_z, (errX.astype(np.int64) @ Hz.T) % 2)
+    np.testing.assert_array_equal(sy_x, (errZ.astype(np.int64) @ Hx.T) % 2)
+
+
+def test_results_table_format():
+    r = {"decSuccessExact": 990, "decSuccessDegen": 0, "DecFailures_X": 3, "DecFailures_Z": 4,
+         "Avg_number_of_iterations_X": 1.25, "Avg_number_of_iterations_Z": 1.5}
+    txt = format_results([0.01], [r], 1000)
+    assert "SIMULATION RESULTS" in txt
+    assert "  1.00e-02  " in txt and "1.00e-02" in txt and "    3,    4" in txt and " 1.25,  1.50" in txt
