@@ -15,6 +15,7 @@
 #include <thread>
 #include <atomic>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -373,6 +374,23 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
       cfg.blocks_per_cu = nb;
       cfg.lds = lds;
     }
+  }
+  // Tuning overrides (experiments only): QLDPC_WAVES_PER_WG, QLDPC_WG_PER_CU.
+  if (const char* ev = getenv("QLDPC_WAVES_PER_WG")) {
+    const int w = atoi(ev);
+    const int lds = blob + w * cfg.wave_bytes;
+    int nb = 0;
+    if (w >= 1 && w <= QLDPC_MAX_THREADS / 64 && lds <= max_lds &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cfg.kernel, 64 * w, (size_t)lds) == hipSuccess && nb > 0) {
+      cfg.waves = w;
+      cfg.blocks_per_cu = nb;
+      cfg.lds = lds;
+      best_waves = nb * w;
+    }
+  }
+  if (const char* ev = getenv("QLDPC_WG_PER_CU")) {
+    const int k = atoi(ev);
+    if (k >= 1 && k < cfg.blocks_per_cu) cfg.blocks_per_cu = k;
   }
   if (best_waves == 0)
     return fail(QLDPC_EUNSUP, "graph needs %d B of LDS per wave plus %d B of tables: exceeds %d B",
