@@ -1,0 +1,86 @@
+"""Throughput of the BASELINE.json configs (and variants) on one GPU.
+
+Each line: decode kernel time per launch and shots/s for one (code, algo,
+schedule, syndrome source) point, with syndromes resident on the device.
+Channel syndromes use the per-qubit Pauli sampler.
+usage: python tools/bench_configs.py [--quick]
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from qldpcsim_amd import _lib, codes, decoders, schedule  # noqa: E402
+
+
+def channel(Hx, Hz, p, B, gen):
+    n = Hx.shape[1]
+    u = torch.rand((B, n), device="cuda", generator=gen)
+    X = u < p / 3
+    Y = (u >= p / 3) & (u < 2 * p / 3)
+    Z = (u >= 2 * p / 3) & (u < p)
+    ex, ez = (X | Y).half(), (Z | Y).half()
+    sz = (ex @ torch.as_tensor(Hz.T, dtype=torch.half, device="cuda")).remainder_(2).to(torch.uint8)
+    sx = (ez @ torch.as_tensor(Hx.T, dtype=torch.half, device="cuda")).remainder_(2).to(torch.uint8)
+    return sz.contiguous(), sx.contiguous()
+
+
+def run(code, algo, sched, p, max_iter, B, reps=2):
+    Hx, Hz = codes.load_code(code)
+    lx, lz = schedule.select_layers(Hx, Hz, sched)
+    gen = torch.Generator(device="cuda").manual_seed(7)
+    if p is None:
+        sz = torch.randint(0, 2, (B, Hz.shape[0]), dtype=torch.uint8, device="cuda", generator=gen)
+        sx = torch.randint(0, 2, (B, Hx.shape[0]), dtype=torch.uint8, device="cuda", generator=gen)
+        prior = 0.05 / 3
+    else:
+        sz, sx = channel(Hx, Hz, p, B, gen)
+        prior = p / 3
+    halves = ((Hz, lx, sz), (Hx, lz, sx))
+    packed = [schedule.pack_layers(l, H.shape[0]) for H, l, _ in halves]
+    for (H, _, s), (lp, lr) in zip(halves, packed):        # warm-up / graph upload
+        decoders.decode_batch(H, s[:1024], prior, max_iter, algo=algo, layer_ptr=lp, layer_rows=lr)
+    torch.cuda.synchronize()
+    _lib.timing_enable(True)
+    _lib.timing_reset()
+    its = 0
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        for (H, _, s), (lp, lr) in zip(halves, packed):
+            r = decoders.decode_batch(H, s, prior, max_iter, algo=algo, layer_ptr=lp, layer_rows=lr)
+            its += int(r.iters.sum().item())
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ms, nl = _lib.timing_read()
+    _lib.timing_enable(False)
+    return {"code": code, "algo": algo, "sched": sched, "p": p, "max_iter": max_iter, "batch": B,
+            "kernel_ms_per_launch": ms / nl, "shots_per_s_kernel": reps * B / (ms / 1e3),
+            "shots_per_s_wall": reps * B / wall, "avg_iters": its / (2 * reps * B)}
+
+
+def main():
+    quick = "--quick" in sys.argv
+    S = 1 << (16 if quick else 18)
+    pts = [
+        ("LP118_0", "MS", "F", None, 50, S * 4),
+        ("LP118_0", "MS", "F", 0.01, 50, S * 4),
+        ("LP118_0", "MS", "F", 0.05, 50, S * 4),
+        ("LP04_0", "MS", "F", 0.05, 50, S * 4),             # configs[1]
+        ("LP118_0", "MS", "L", None, 50, S),
+        ("LP118_0", "BP", "F", 0.05, 100, S),                # configs[2]
+        ("LP118_0", "BP", "L", 0.05, 100, S),
+        ("LP118_0", "BP", "F", None, 100, S // 4),
+        ("LP118_2", "MS", "L", 0.05, 50, S),                 # configs[3] (decoder part)
+        ("LP118_2", "MS", "F", None, 50, S),
+        ("LP118_2", "BP", "L", 0.05, 100, S // 2),           # configs[4] (decoder part)
+    ]
+    for pt in pts:
+        print(json.dumps(run(*pt)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
