@@ -1,0 +1,60 @@
+"""End-to-end simulator on the GPU: counters equal a per-shot restatement of
+simulator.py:244-315 driven by the oracle decoders on the same samples; the
+CLI runs and prints the reference's table."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("code,decType,sched,osd,p", [
+    ("LP04_0", "MS", "F", -1, 0.1),
+    ("LP04_0", "MS", "L", 0, 0.12),
+    ("LP118_0", "MS", "F", -1, 0.06),
+    ("LP04_0", "BP", "L", 4, 0.1),      # BP ignores OSDorder in simulate (simulator.py:281-282)
+])
+def test_simulate_p_counters_match_oracle_restatement(code, decType, sched, osd, p):
+    from oracle import oracle
+    from qldpcsim_amd import codes, schedule, simulator
+    Hx, Hz = codes.load_code(code)
+    shots = 3000
+    smp = simulator.sample_channel(Hx, Hz, p, shots, np.random.default_rng(17))
+    got = simulator.simulate_p(Hx, Hz, p, shots=shots, decType=decType, decIterations=30,
+                               decSchedule=sched, OSDorder=osd, samples=smp, batch_size=1000,
+                               verbose=False)
+    lx, lz = schedule.select_layers(Hx, Hz, sched)
+    sy_z, sy_x, errX, errZ = smp
+    outs = []
+    for H, layers, syn in ((Hz, lx, sy_z), (Hx, lz, sy_x)):
+        lp, lr = schedule.pack_layers(layers, H.shape[0])
+        e, it, post, _ = oracle.decode_batch(decType, H, syn, p / 3, 30, lp, lr)
+        if decType == "MS" and osd >= 0:
+            for k in range(shots):
+                if not np.all((H.astype(np.int64) @ e[k]) % 2 == syn[k]):
+                    e[k] = oracle.osd_dec(H, e[k].astype(np.int64), syn[k].astype(np.int64),
+                                          post[k], osd).astype(np.uint8)
+        outs.append((e, it))
+    (eX, itX), (eZ, itZ) = outs
+    want = dict(DecFailures_X=0, DecFailures_Z=0, decSuccessExact=0, decSuccessDegen=0)
+    for k in range(shots):
+        if np.array_equal(errX[k], eX[k]) and np.array_equal(errZ[k], eZ[k]):
+            want["decSuccessExact"] += 1
+        elif ((Hz @ (errX[k].astype(int) ^ eX[k])) == 0).all() and ((Hx @ (errZ[k].astype(int) ^ eZ[k])) == 0).all():
+            want["decSuccessDegen"] += 1
+        want["DecFailures_X"] += int(not np.array_equal(sy_z[k], (Hz.astype(int) @ eX[k]) % 2))
+        want["DecFailures_Z"] += int(not np.array_equal(sy_x[k], (Hx.astype(int) @ eZ[k]) % 2))
+    want["Avg_number_of_iterations_X"] = itX.sum() / float(shots)
+    want["Avg_number_of_iterations_Z"] = itZ.sum() / float(shots)
+    assert got == want
+
+
+def test_cli_main_prints_reference_table(tmp_path, capsys):
+    from qldpcsim_amd import codes, simulator
+    Hx, Hz = codes.load_code("LP04_0")
+    np.save(tmp_path / "Hx.npy", Hx.astype(np.int64))
+    np.save(tmp_path / "Hz.npy", Hz.astype(np.int64))
+    simulator.main(["--Hx", str(tmp_path / "Hx.npy"), "--Hz", str(tmp_path / "Hz.npy"),
+                    "--p", "0.02", "0.08", "--shots", "2000", "--decType", "MS",
+                    "--decIterations", "30", "--decSchedule", "L", "--rngSeed", "5"])
+    out = capsys.readouterr().out
+    assert "SIMULATION RESULTS" in out and "2.00e-02" in out and "8.00e-02" in out
