@@ -354,7 +354,13 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   }
   const qldpc_code* c = s->code;
   const int dc = fast_table_ok(c) ? c->uniform_deg : 0;
-  cfg.kernel = qldpc::select_kernel(algo, s->layered, dc);
+  cfg.kernel = nullptr;
+  int max_waves = QLDPC_MAX_THREADS / 64;
+  if (algo == QLDPC_ALGO_MS && !s->layered && dc > 0 && !getenv("QLDPC_NO_REGTAB")) {
+    cfg.kernel = qldpc::select_ms_flood_kernel(dc, (c->m + 63) / 64, (c->n + 63) / 64);
+    if (cfg.kernel) max_waves = qldpc::ms_flood_max_waves((c->m + 63) / 64);
+  }
+  if (!cfg.kernel) cfg.kernel = qldpc::select_kernel(algo, s->layered, dc);
   int off_c2v, off_synw, off_parw;
   wave_layout(c, s->layered, algo, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw);
   int max_lds = 0, dev = 0;
@@ -363,7 +369,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   HIP_TRY(qldpc::configure_kernel(cfg.kernel, max_lds));
   const int blob = (int)s->blob.size();
   int best_waves = 0;
-  for (int w = QLDPC_MAX_THREADS / 64; w >= 1; --w) {
+  for (int w = max_waves; w >= 1; --w) {
     const int lds = blob + w * cfg.wave_bytes;
     if (lds > max_lds) continue;
     int nb = 0;
@@ -380,7 +386,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
     const int w = atoi(ev);
     const int lds = blob + w * cfg.wave_bytes;
     int nb = 0;
-    if (w >= 1 && w <= QLDPC_MAX_THREADS / 64 && lds <= max_lds &&
+    if (w >= 1 && w <= max_waves && lds <= max_lds &&
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cfg.kernel, 64 * w, (size_t)lds) == hipSuccess && nb > 0) {
       cfg.waves = w;
       cfg.blocks_per_cu = nb;

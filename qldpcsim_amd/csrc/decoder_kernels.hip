@@ -102,6 +102,18 @@ __device__ __forceinline__ int tab_var(uint32_t t) { return DC ? (int)((t & 0xff
 template <int DC>
 __device__ __forceinline__ int tab_pos(uint32_t t) { return DC ? (int)(t >> 18) : (int)(t & 0xffffu); }
 
+// Hide a register value's provenance from the optimizer: values derived from
+// it (addresses, predicates) are then recomputed where used instead of being
+// hoisted out of the persistent loop, which would cost one VGPR each.
+template <int WHICH>  // 1: check-node table words, 2: variable-node words
+__device__ __forceinline__ uint32_t opaque(uint32_t x) {
+#ifndef QLDPC_OPAQUE_MASK
+#define QLDPC_OPAQUE_MASK 2  // hoist check-node addresses (measured fastest), recompute VN ones
+#endif
+  if constexpr ((QLDPC_OPAQUE_MASK & WHICH) != 0) asm volatile("" : "+v"(x));
+  return x;
+}
+
 __device__ __forceinline__ uint32_t hi_word(double d) { return (uint32_t)(__builtin_bit_cast(uint64_t, d) >> 32); }
 
 // ---------------------------------------------------------------------------
@@ -114,22 +126,21 @@ __device__ __forceinline__ uint32_t hi_word(double d) { return (uint32_t)(__buil
 // (v_e is never -0.0 and post never -0.0 or NaN for finite L: DESIGN.md §4).
 // Returns the check's "unsatisfied" bit for the posteriors it read.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ void load_row8(const uint32_t* tab, uint32_t (&t)[8]) {
+  const uint4 t0 = *(const uint4*)tab;
+  const uint4 t1 = *(const uint4*)(tab + 4);
+  t[0] = t0.x; t[1] = t0.y; t[2] = t0.z; t[3] = t0.w;
+  t[4] = t1.x; t[5] = t1.y; t[6] = t1.z; t[7] = t1.w;
+}
+
+// NC independent checks per call: every LDS read of all NC checks is issued
+// before any arithmetic. `t[q]` holds check q's 8 table words (registers).
 template <int DC, bool FIRST, int NC>
-__device__ __forceinline__ uint32_t cn_ms_uniform(const DecodeArgs& a, const uint32_t* const* tabs,
+__device__ __forceinline__ uint32_t cn_ms_uniform(const DecodeArgs& a, const uint32_t (*t)[8],
                                                   const uint32_t* synb, const bool* live,
                                                   const unsigned char* post_b,
                                                   unsigned char* c2v_b, int& fl) {
-  // NC independent checks per call: every LDS read of all NC checks is issued
-  // before any arithmetic, so a wave keeps 2*DC*NC reads in flight.
   static_assert(DC >= 2 && DC <= 8, "uniform fast path handles row degrees 2..8");
-  uint32_t t[NC][8];
-#pragma unroll
-  for (int q = 0; q < NC; ++q) {
-    const uint4 t0 = *(const uint4*)tabs[q];
-    const uint4 t1 = *(const uint4*)(tabs[q] + 4);
-    t[q][0] = t0.x; t[q][1] = t0.y; t[q][2] = t0.z; t[q][3] = t0.w;
-    t[q][4] = t1.x; t[q][5] = t1.y; t[q][6] = t1.z; t[q][7] = t1.w;
-  }
   if constexpr (FIRST) {
     // every v_e = float32(L): min1 = min2 = |L32|, argmin 0, sign_e = L32 < 0
     const double vf = (double)a.L32;
@@ -206,11 +217,12 @@ __device__ __forceinline__ uint32_t cn_update(const DecodeArgs& a, const LdsView
                                               uint32_t synb, bool first, const double* post,
                                               void* c2v_raw, int& fl) {
   if constexpr (ALGO == ALGO_MS && DC > 0) {
-    const uint32_t* tabs[1] = {g.cn_tab + c * 8};
+    uint32_t t[1][8];
+    load_row8(g.cn_tab + c * 8, t[0]);
     const uint32_t sb[1] = {synb};
     const bool live[1] = {true};
-    if (first) return cn_ms_uniform<DC, true, 1>(a, tabs, sb, live, (const unsigned char*)post, (unsigned char*)c2v_raw, fl);
-    return cn_ms_uniform<DC, false, 1>(a, tabs, sb, live, (const unsigned char*)post, (unsigned char*)c2v_raw, fl);
+    if (first) return cn_ms_uniform<DC, true, 1>(a, t, sb, live, (const unsigned char*)post, (unsigned char*)c2v_raw, fl);
+    return cn_ms_uniform<DC, false, 1>(a, t, sb, live, (const unsigned char*)post, (unsigned char*)c2v_raw, fl);
   }
   const int e0 = DC ? c * 8 : (int)g.row_ptr[c];
   const int deg = DC ? DC : (int)g.row_ptr[c + 1] - e0;
@@ -409,16 +421,15 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) decode_kernel(DecodeArgs a)
         if constexpr (QLDPC_ABLATE == 2) {
           unsat = 1;
         } else if constexpr (ALGO == ALGO_MS && DC > 0) {
-          // two checks (c, c + 64) per lane per step; a missing second check
-          // re-reads check c's row (in bounds) and skips its stores
           for (int i = 0, c = lane; c < m; ++i, c += 64) {
-            const uint32_t* tabs[1] = {g.cn_tab + c * 8};
+            uint32_t t[1][8];
+            load_row8(g.cn_tab + c * 8, t[0]);
             const uint32_t sb[1] = {(synreg >> i) & 1u};
             const bool live[1] = {true};
             if (it == 0)
-              (void)cn_ms_uniform<DC, true, 1>(a, tabs, sb, live, (const unsigned char*)post, (unsigned char*)c2v, fl);
+              (void)cn_ms_uniform<DC, true, 1>(a, t, sb, live, (const unsigned char*)post, (unsigned char*)c2v, fl);
             else
-              unsat |= cn_ms_uniform<DC, false, 1>(a, tabs, sb, live, (const unsigned char*)post, (unsigned char*)c2v, fl);
+              unsat |= cn_ms_uniform<DC, false, 1>(a, t, sb, live, (const unsigned char*)post, (unsigned char*)c2v, fl);
           }
         } else if (it == 0) {
           for (int i = 0, c = lane; c < m; ++i, c += 64)
@@ -544,11 +555,179 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) decode_kernel(DecodeArgs a)
 }
 
 // ---------------------------------------------------------------------------
+// Flooding min-sum for uniform-degree codes with the lane's static graph data
+// held in VGPRs for the whole (persistent) kernel: the 8 table words of each
+// of its <= KC checks and the CSC start|degree word of each of its <= VP
+// variables. Each check-node step is then one LDS round trip (the gathers)
+// and each variable-node pass one round trip (the column). Same arithmetic
+// and results as decode_kernel<MS, false, DC>.
+// ---------------------------------------------------------------------------
+template <int K>
+__device__ __forceinline__ float ms_colsum_sw(const float* c, int d, int dmax) {
+  switch (dmax) {
+    case 0: return 0.0f;
+    case 1: return ms_colsum<1>(c, d);
+    case 2: return ms_colsum<2>(c, d);
+    case 3: return ms_colsum<3>(c, d);
+    case 4: return ms_colsum<4>(c, d);
+    case 5: return ms_colsum<5>(c, d);
+    case 6: return ms_colsum<6>(c, d);
+    case 7: return ms_colsum<7>(c, d);
+    case 8: return ms_colsum<8>(c, d);
+    default: {
+      float s = 0.0f;
+      for (int t = 0; t < d; ++t) s += c[t];
+      return s;
+    }
+  }
+}
+
+// Large codes (KC = 8 checks per lane) keep 64 table words in VGPRs; their
+// per-wave LDS slice allows <= 2 waves per SIMD anyway, so they are compiled
+// for 512-thread workgroups (256 VGPRs) instead of 768.
+template <int KC>
+constexpr int ms_flood_max_threads() { return KC >= 8 ? 512 : QLDPC_MAX_THREADS; }
+
+template <int DC, int KC, int VP>
+__global__ void __launch_bounds__(ms_flood_max_threads<KC>()) ms_flood_kernel(DecodeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  {
+    const uint4* src = (const uint4*)a.blob;
+    uint4* dst = (uint4*)lds;
+    const int nvec = a.blob_bytes >> 4;
+    for (int i = threadIdx.x; i < nvec; i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  const uint32_t* cn_tab = (const uint32_t*)(lds + a.off_cn_tab);
+  const uint32_t* vn_info = (const uint32_t*)(lds + a.off_vn_ptr);
+  const uint8_t* chunk_dmax = (const uint8_t*)(lds + a.off_chunk_dmax);
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int waves = blockDim.x >> 6;
+  unsigned char* ws = lds + a.blob_bytes + wid * a.wave_bytes;
+  double* post = (double*)ws;
+  unsigned char* c2v_b = ws + a.off_c2v;
+  const float* c2v_f = (const float*)c2v_b;
+  const int m = a.m, n = a.n;
+
+  // static per-lane graph data (registers for the whole kernel)
+  uint32_t tr[KC][8];
+#pragma unroll
+  for (int i = 0; i < KC; ++i) {
+    const int c = lane + 64 * i;
+    load_row8(cn_tab + (c < m ? c : m - 1) * 8, tr[i]);
+  }
+  uint32_t vi[VP];
+  int dm[VP];
+#pragma unroll
+  for (int q = 0; q < VP; ++q) {
+    const int j = lane + 64 * q;
+    vi[q] = j < n ? vn_info[j] : 0u;
+    dm[q] = 64 * q < n ? __builtin_amdgcn_readfirstlane((int)chunk_dmax[q]) : 0;
+  }
+
+  for (long long hs = (long long)blockIdx.x * waves + wid; hs < a.batch;
+       hs += (long long)gridDim.x * waves) {
+    const uint8_t* syn = a.syn + hs * (long long)m;
+    int fl = 0;
+    int iters = a.max_iter;
+    bool conv = false;
+    uint32_t synreg = 0;
+#pragma unroll
+    for (int i = 0; i < KC; ++i) {
+      const int c = lane + 64 * i;
+      if (c < m) synreg |= (uint32_t)(syn[c] & 1) << i;
+    }
+    for (int it = 0;; ++it) {
+      uint32_t unsat = 0;
+      if (it == 0) {
+#pragma unroll
+        for (int i = 0; i < KC; ++i) {
+          const bool live[1] = {lane + 64 * i < m};
+          const uint32_t sb[1] = {(synreg >> i) & 1u};
+          uint32_t t[1][8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) t[0][k] = opaque<1>(tr[i][k]);
+          (void)cn_ms_uniform<DC, true, 1>(a, t, sb, live, (const unsigned char*)post, c2v_b, fl);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < KC; ++i) {
+          const bool live[1] = {lane + 64 * i < m};
+          const uint32_t sb[1] = {(synreg >> i) & 1u};
+          uint32_t t[1][8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) t[0][k] = opaque<1>(tr[i][k]);
+          unsat |= cn_ms_uniform<DC, false, 1>(a, t, sb, live, (const unsigned char*)post, c2v_b, fl);
+          __builtin_amdgcn_sched_barrier(0);         // one check's working set at a time
+        }
+        // stop test of iteration it-1 (decoders.py:175-176)
+        if (ballot(unsat != 0) == 0) {
+          iters = it;
+          conv = true;
+          break;
+        }
+      }
+      wave_sync();
+#pragma unroll
+      for (int q = 0; q < VP; ++q) {
+        if (64 * q < n) {                            // wave-uniform
+          const int j = lane + 64 * q;
+          const uint32_t w = opaque<2>(vi[q]);
+          const float s = ms_colsum_sw<0>(c2v_f + (w & 0xffffu), (int)(w >> 16), dm[q]);
+          if (j < n) post[j] = a.L + (double)s;      // (:172-173)
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      wave_sync();
+      if (it + 1 == a.max_iter) {
+        uint32_t un = 0;
+#pragma unroll
+        for (int i = 0; i < KC; ++i) {
+          uint32_t ph = 0;
+#pragma unroll
+          for (int k = 0; k < DC; ++k) ph ^= hi_word(*(const double*)((const unsigned char*)post + (opaque<1>(tr[i][k]) & 0xffffu)));
+          if (lane + 64 * i < m) un |= (ph >> 31) ^ ((synreg >> i) & 1u);
+        }
+        conv = ballot(un != 0) == 0;
+        break;
+      }
+    }
+    uint8_t* eh = a.ehat + hs * (long long)n;
+    double* po = a.post ? a.post + hs * (long long)n : nullptr;
+    for (int jo = lane; jo < n; jo += 64) {
+      const double pv = post[a.vinv[jo]];
+      eh[jo] = (uint8_t)(pv < 0.0);
+      if (po) po[jo] = pv;
+    }
+    const uint64_t b1 = ballot((fl & FLAG_MIN_ZERO) != 0);
+    if (lane == 0) {
+      a.iters[hs] = iters;
+      if (a.flags) a.flags[hs] = (int32_t)((b1 ? FLAG_MIN_ZERO : 0) | (conv ? FLAG_CONVERGED : 0));
+    }
+    wave_sync();
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Host-side launch helpers (called from capi.cpp)
 // ---------------------------------------------------------------------------
 template <int ALGO, bool LAYERED, int DC>
 static const void* kernel_ptr() {
   return (const void*)&decode_kernel<ALGO, LAYERED, DC>;
+}
+
+int ms_flood_max_waves(int kc) { return (kc > 4 ? 512 : QLDPC_MAX_THREADS) / 64; }
+
+const void* select_ms_flood_kernel(int dc, int kc, int vp) {
+  // instantiated (DC, KC, VP) shapes; the host passes the smallest that covers
+  // ceil(m/64) checks and ceil(n/64) variable passes per lane
+  if (dc == 7 && kc <= 2 && vp <= 4) return (const void*)&ms_flood_kernel<7, 2, 4>;
+  if (dc == 7 && kc <= 4 && vp <= 9) return (const void*)&ms_flood_kernel<7, 4, 9>;
+  if (dc == 8 && kc <= 4 && vp <= 9) return (const void*)&ms_flood_kernel<8, 4, 9>;
+  if (dc == 7 && kc <= 8 && vp <= 17) return (const void*)&ms_flood_kernel<7, 8, 17>;
+  if (dc == 8 && kc <= 8 && vp <= 17) return (const void*)&ms_flood_kernel<8, 8, 17>;
+  return nullptr;
 }
 
 const void* select_kernel(int algo, bool layered, int dc) {
