@@ -105,6 +105,78 @@ def count_outcomes(Hx, Hz, sy_z, sy_x, errX, errZ, eX, eZ, itX, itZ):
     }
 
 
+class DeviceChannel:
+    """Device-side depolarizing sampler and outcome counters (torch on the HIP
+    device): the same per-qubit draw as `sample_channel` and the same counter
+    definitions as `count_outcomes`, without moving shots through host memory.
+    Syndromes are H·e mod 2 from an fp16 GEMM (exact: at most row-weight
+    nonzero products per entry)."""
+
+    def __init__(self, Hx, Hz, device, seed):
+        import torch
+        self.torch = torch
+        self.dev = device
+        self.HxT = torch.as_tensor(Hx.T, dtype=torch.half, device=device).contiguous()
+        self.HzT = torch.as_tensor(Hz.T, dtype=torch.half, device=device).contiguous()
+        self.n = Hx.shape[1]
+        self.gen = torch.Generator(device=device)
+        self.gen.manual_seed(int(seed) & ((1 << 63) - 1))
+
+    def sample(self, p, B):
+        torch = self.torch
+        u = torch.rand((B, self.n), device=self.dev, generator=self.gen)
+        q = p / 3
+        X = u < q
+        Y = (u >= q) & (u < 2 * q)
+        Z = (u >= 2 * q) & (u < p)
+        errX = (X | Y).to(torch.uint8)
+        errZ = (Z | Y).to(torch.uint8)
+        sy_z = self._syn(errX, self.HzT)
+        sy_x = self._syn(errZ, self.HxT)
+        return sy_z, sy_x, errX, errZ
+
+    @staticmethod
+    def _syn(e, HT):
+        return (e.half() @ HT).to(dtype=e.dtype) & 1
+
+    def count(self, sy_z, sy_x, errX, errZ, eX, eZ, itX, itZ):
+        torch = self.torch
+        exact = (errX == eX).all(dim=1) & (errZ == eZ).all(dim=1)
+        # integer products (no mod 2), as simulator.py:296
+        zX = ((errX ^ eX).half() @ self.HzT == 0).all(dim=1)
+        zZ = ((errZ ^ eZ).half() @ self.HxT == 0).all(dim=1)
+        degen = (~exact) & zX & zZ
+        failX = (self._syn(eX, self.HzT) != sy_z).any(dim=1)
+        failZ = (self._syn(eZ, self.HxT) != sy_x).any(dim=1)
+        v = torch.stack([failX.sum(), failZ.sum(), exact.sum(), degen.sum(),
+                         itX.to(torch.int64).sum(), itZ.to(torch.int64).sum()]).cpu().tolist()
+        return dict(zip(COUNTER_KEYS, (int(x) for x in v)))
+
+
+def _osd_on_device_result(H, syn_d, r, order):
+    """OSD post-step (decoders.py:179-180) for the non-converged shots of a
+    device decode: only those rows travel to the host."""
+    import torch
+    from . import _lib
+    bad = ((r.flags & _lib.FLAG_CONVERGED) == 0).nonzero().flatten()
+    if bad.numel() == 0:
+        return
+    syn = syn_d[bad].cpu().numpy()
+    e = r.ehat[bad].cpu().numpy()
+    post = r.post[bad].cpu().numpy()
+    flags = np.zeros(len(e), np.int32)
+    decoders.apply_osd(H, syn, e, post, flags, order)
+    r.ehat[bad] = torch.as_tensor(e, device=r.ehat.device)
+
+
+def _device_ok():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except ImportError:
+        return False
+
+
 def _dist():
     try:
         import torch.distributed as dist
@@ -118,12 +190,14 @@ def _dist():
 def simulate_p(Hx: np.ndarray, Hz: np.ndarray, p: float, shots: int = 1000, decType: str = "MS",
                decIterations: int = 99, decSchedule: str = "F", OSDorder: int = -1,
                rngSeed: Optional[int] = None, *, batch_size: int = 1 << 16,
-               verbose: bool = True, samples=None) -> dict:
+               verbose: bool = True, samples=None, sampler: Optional[str] = None) -> dict:
     """One depolarizing probability: sample, decode both halves, count.
 
     Returns the reference's dict (simulator.py:308-315). `samples`, if given,
     is a tuple (sy_z, sy_x, errX, errZ) to decode instead of sampling (used by
-    the parity tests). Extra keyword arguments default to reference behaviour.
+    the parity tests). `sampler`: "device" (torch RNG + counters on the GPU,
+    the default when a device is present), or "host" (NumPy). Extra keyword
+    arguments default to reference behaviour.
     """
     if rngSeed is not None:
         np.random.seed(rngSeed)                    # reference side effect (:187-188)
@@ -153,18 +227,35 @@ def simulate_p(Hx: np.ndarray, Hz: np.ndarray, p: float, shots: int = 1000, decT
     tot = {k: 0 for k in COUNTER_KEYS}
     t0 = time.time()
     done = 0
+    use_dev = sampler == "device" or (sampler is None and samples is None and _device_ok())
+    if use_dev:
+        import torch
+        dev = torch.device("cuda", torch.cuda.current_device())
+        ch = DeviceChannel(Hx, Hz, dev, np.random.SeedSequence(seed).generate_state(1, np.uint64)[0])
     while done < my_shots:
         B = min(batch_size, my_shots - done)
-        if samples is not None:
+        if use_dev:
+            sy_z, sy_x, errX, errZ = ch.sample(p, B)
+            want_post = osd >= 0
+            rX = decoders.decode_batch(Hz, sy_z, p / 3, decIterations, algo=decType, want_post=want_post,
+                                       layer_ptr=lpX, layer_rows=lrX)
+            rZ = decoders.decode_batch(Hx, sy_x, p / 3, decIterations, algo=decType, want_post=want_post,
+                                       layer_ptr=lpZ, layer_rows=lrZ)
+            if osd >= 0:
+                _osd_on_device_result(Hz, sy_z, rX, osd)
+                _osd_on_device_result(Hx, sy_x, rZ, osd)
+            c = ch.count(sy_z, sy_x, errX, errZ, rX.ehat, rZ.ehat, rX.iters, rZ.iters)
+        elif samples is not None:
             sl = slice(my_start + done, my_start + done + B)
             sy_z, sy_x, errX, errZ = (np.asarray(a)[sl].astype(np.uint8) for a in samples)
         else:
             sy_z, sy_x, errX, errZ = sample_channel(Hx, Hz, p, B, rng)
-        rX = decoders.decode_batch(Hz, sy_z, p / 3, decIterations, algo=decType, osd_order=osd,
-                                   layer_ptr=lpX, layer_rows=lrX)
-        rZ = decoders.decode_batch(Hx, sy_x, p / 3, decIterations, algo=decType, osd_order=osd,
-                                   layer_ptr=lpZ, layer_rows=lrZ)
-        c = count_outcomes(Hx, Hz, sy_z, sy_x, errX, errZ, rX.ehat, rZ.ehat, rX.iters, rZ.iters)
+        if not use_dev:
+            rX = decoders.decode_batch(Hz, sy_z, p / 3, decIterations, algo=decType, osd_order=osd,
+                                       layer_ptr=lpX, layer_rows=lrX)
+            rZ = decoders.decode_batch(Hx, sy_x, p / 3, decIterations, algo=decType, osd_order=osd,
+                                       layer_ptr=lpZ, layer_rows=lrZ)
+            c = count_outcomes(Hx, Hz, sy_z, sy_x, errX, errZ, rX.ehat, rZ.ehat, rX.iters, rZ.iters)
         for k in tot:
             tot[k] += c[k]
         done += B
@@ -208,7 +299,7 @@ def format_results(p, results, shots):
 def simulate(HxFile: str, HzFile: str, p, shots: int = 1000, decType: str = "MS",
              decIterations: int = 99, decSchedule: str = "F", OSDorder: int = -1,
              rngSeed: Optional[int] = None, *, batch_size: int = 1 << 16, verbose: bool = True,
-             return_results: bool = False):
+             return_results: bool = False, sampler: Optional[str] = None):
     """p-sweep + results table (simulator.py:319-347). Returns None like the
     reference unless return_results=True."""
     Hx = load_matrix(HxFile)
@@ -218,7 +309,8 @@ def simulate(HxFile: str, HzFile: str, p, shots: int = 1000, decType: str = "MS"
     for pT in p:
         results.append(simulate_p(Hx, Hz, p=pT, shots=shots, rngSeed=rngSeed, decType=decType,
                                   decIterations=decIterations, decSchedule=decSchedule,
-                                  OSDorder=OSDorder, batch_size=batch_size, verbose=verbose))
+                                  OSDorder=OSDorder, batch_size=batch_size, verbose=verbose,
+                                  sampler=sampler))
     _, rank, _ = _dist()
     if rank == 0:
         print(format_results(p, results, shots))
@@ -239,13 +331,16 @@ def main(argv=None):
                         help="Decoder scheduling method: [F] flooding; [L] layered; [S] serial.")
     parser.add_argument("--OSDorder", type=int, default=-1, help="Ordered Statistics Decoding order.")
     parser.add_argument("--batch", type=int, default=1 << 16, help="Shots per GPU batch.")
+    parser.add_argument("--sampler", choices=["device", "host"], default=None,
+                        help="Where shots are sampled and counted (default: device if present).")
     args = parser.parse_args(argv)
     print("\n   Command line arguments:")
     print(args)
     print("")
     simulate(HxFile=args.Hx, HzFile=args.Hz, p=args.p, shots=args.shots, decType=args.decType,
              decIterations=args.decIterations, decSchedule=args.decSchedule,
-             OSDorder=args.OSDorder, rngSeed=args.rngSeed, batch_size=args.batch)
+             OSDorder=args.OSDorder, rngSeed=args.rngSeed, batch_size=args.batch,
+             sampler=args.sampler)
 
 
 if __name__ == "__main__":

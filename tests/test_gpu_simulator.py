@@ -58,3 +58,41 @@ def test_cli_main_prints_reference_table(tmp_path, capsys):
                     "--decIterations", "30", "--decSchedule", "L", "--rngSeed", "5"])
     out = capsys.readouterr().out
     assert "SIMULATION RESULTS" in out and "2.00e-02" in out and "8.00e-02" in out
+
+
+def test_device_channel_counters_equal_host_counters():
+    """DeviceChannel's sampler statistics and its on-device counters equal the
+    host restatement (count_outcomes) on the same device-drawn shots."""
+    import torch
+    from qldpcsim_amd import codes, decoders, simulator
+    Hx, Hz = codes.load_code("LP118_0")
+    ch = simulator.DeviceChannel(Hx, Hz, torch.device("cuda", 0), 123)
+    p = 0.06
+    sy_z, sy_x, errX, errZ = ch.sample(p, 50000)
+    ex = errX.cpu().numpy()
+    assert abs(ex.mean() - 2 * p / 3) < 0.002
+    np.testing.assert_array_equal(sy_z.cpu().numpy(), (ex.astype(np.int64) @ Hz.T) % 2)
+    rX = decoders.decode_batch(Hz, sy_z, p / 3, 30)
+    rZ = decoders.decode_batch(Hx, sy_x, p / 3, 30)
+    dev = ch.count(sy_z, sy_x, errX, errZ, rX.ehat, rZ.ehat, rX.iters, rZ.iters)
+    host = simulator.count_outcomes(Hx, Hz, sy_z.cpu().numpy(), sy_x.cpu().numpy(), ex,
+                                    errZ.cpu().numpy(), rX.ehat.cpu().numpy(), rZ.ehat.cpu().numpy(),
+                                    rX.iters.cpu().numpy(), rZ.iters.cpu().numpy())
+    assert dev == host
+
+
+def test_device_sampler_simulate_p_with_osd_agrees_with_host_sampler():
+    """Same code/decoder through both samplers: counter rates agree within
+    sampling error; OSD on the device path leaves no decoding failure where
+    OSD applies (its solve always satisfies a valid syndrome)."""
+    from qldpcsim_amd import codes, simulator
+    Hx, Hz = codes.load_code("LP04_0")
+    kw = dict(shots=20000, decType="MS", decIterations=20, decSchedule="F", rngSeed=3,
+              batch_size=8192, verbose=False)
+    d = simulator.simulate_p(Hx, Hz, 0.1, OSDorder=0, sampler="device", **kw)
+    h = simulator.simulate_p(Hx, Hz, 0.1, OSDorder=0, sampler="host", **kw)
+    assert d["DecFailures_X"] == 0 and d["DecFailures_Z"] == 0
+    assert h["DecFailures_X"] == 0 and h["DecFailures_Z"] == 0
+    for k in ("decSuccessExact",):
+        assert abs(d[k] - h[k]) < 5 * np.sqrt(kw["shots"] * 0.25)
+    assert abs(d["Avg_number_of_iterations_X"] - h["Avg_number_of_iterations_X"]) < 0.2
