@@ -123,6 +123,15 @@ int qldpc_osd_decode(const qldpc_code *code, const uint8_t *h_syn, const int32_t
 int qldpc_osd_decode_batch(const qldpc_code *code, int64_t count, const uint8_t *h_syn,
                            const int32_t *h_perm, int order, uint8_t *h_ehat, int nthreads);
 
+/* Batched OSD on the device: one workgroup per shot, asynchronous on `stream`.
+ * Same semantics as qldpc_osd_decode (orders 0, 1, >= 2) for `count` shots:
+ * d_syn uint8[count][m], d_perm int32[count][n] (NumPy's reliability order),
+ * d_ehat uint8[count][n] in/out, d_status int32[count] (0 ok; 1 = the
+ * reference's IndexError case, e_hat left unchanged). m <= 1024, n <= 2111. */
+int qldpc_osd_device(const qldpc_code *code, int64_t count, const uint8_t *d_syn,
+                     const int32_t *d_perm, int order, uint8_t *d_ehat, int32_t *d_status,
+                     void *stream);
+
 /* First element of CPython's `set(range(n)) - set(J)` iteration order
  * (the reference's infoSet[0], decoders.py:344); -1 if empty. */
 int qldpc_cpython_setdiff_first(int n, const int32_t *J, int nJ);

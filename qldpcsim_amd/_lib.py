@@ -23,7 +23,7 @@ EXPORTS = (
     "qldpc_code_create", "qldpc_code_destroy", "qldpc_code_shape",
     "qldpc_schedule_create", "qldpc_schedule_destroy",
     "qldpc_decode_device", "qldpc_decode_host",
-    "qldpc_osd_decode", "qldpc_osd_decode_batch", "qldpc_cpython_setdiff_first",
+    "qldpc_osd_decode", "qldpc_osd_decode_batch", "qldpc_osd_device", "qldpc_cpython_setdiff_first",
     "qldpc_timing_enable", "qldpc_timing_reset", "qldpc_timing_read",
 )
 
@@ -62,6 +62,7 @@ def _load():
         "qldpc_decode_host": ([P, P, I, P, I64, D, I, D, D, P, P, P, P], I),
         "qldpc_osd_decode": ([P, P, P, I, P, P, P, I], I),
         "qldpc_osd_decode_batch": ([P, I64, P, P, I, P, I], I),
+        "qldpc_osd_device": ([P, I64, P, P, I, P, P, P], I),
         "qldpc_cpython_setdiff_first": ([I, P, I], I),
         "qldpc_timing_enable": ([I], I),
         "qldpc_timing_reset": ([], I),

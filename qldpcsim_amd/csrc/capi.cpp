@@ -24,6 +24,7 @@
 
 #include "../../include/qldpc_decoder.h"
 #include "decoder_kernels.h"
+#include "osd_kernels.h"
 
 using qldpc::DecodeArgs;
 
@@ -74,6 +75,7 @@ struct qldpc_code {
   int mw = 0;                                // 64-bit words per column bit-vector
   std::vector<uint64_t> col_bits;            // [n][mw] column j of H (OSD)
   uint16_t* d_vinv = nullptr;
+  int32_t *d_row_ptr = nullptr, *d_col_idx = nullptr;  // CSR for the GPU OSD
   // host staging workspace for qldpc_decode_host
   std::mutex ws_mu;
   int64_t ws_cap = 0;
@@ -146,6 +148,10 @@ extern "C" int qldpc_code_create(const uint8_t* h_H, int m, int n, qldpc_code** 
     std::vector<uint16_t> v16(c->vinv.begin(), c->vinv.end());
     hipError_t e1 = hipMalloc(&c->d_vinv, sizeof(uint16_t) * n);
     if (e1 == hipSuccess) e1 = hipMemcpy(c->d_vinv, v16.data(), sizeof(uint16_t) * n, hipMemcpyHostToDevice);
+    if (e1 == hipSuccess) e1 = hipMalloc(&c->d_row_ptr, sizeof(int32_t) * (m + 1));
+    if (e1 == hipSuccess) e1 = hipMemcpy(c->d_row_ptr, c->row_ptr.data(), sizeof(int32_t) * (m + 1), hipMemcpyHostToDevice);
+    if (e1 == hipSuccess) e1 = hipMalloc(&c->d_col_idx, sizeof(int32_t) * std::max(1, c->E));
+    if (e1 == hipSuccess && c->E) e1 = hipMemcpy(c->d_col_idx, c->col_idx.data(), sizeof(int32_t) * c->E, hipMemcpyHostToDevice);
     if (e1 != hipSuccess) {
       delete c;
       return fail(QLDPC_EHIP, "uploading the graph failed: %s", hipGetErrorString(e1));
@@ -170,6 +176,8 @@ static void ws_free(qldpc_code* c) {
 extern "C" int qldpc_code_destroy(qldpc_code* code) {
   if (!code) return QLDPC_OK;
   (void)hipFree(code->d_vinv);
+  (void)hipFree(code->d_row_ptr);
+  (void)hipFree(code->d_col_idx);
   ws_free(code);
   delete code;
   return QLDPC_OK;
@@ -826,4 +834,71 @@ extern "C" int qldpc_osd_decode_batch(const qldpc_code* code, int64_t count, con
   for (auto& t : th) t.join();
   if (rc.load() != QLDPC_OK) g_err = err;
   return rc.load();
+}
+
+// ---------------------------------------------------------------------------
+// GPU OSD (osd_kernels.hip): one workgroup per shot.
+// ---------------------------------------------------------------------------
+static int setdiff_table_ints(int n) {
+  // largest (new table + old table) CPython's set reaches inserting n keys
+  size_t mask = 7, fill = 0, best = 16;
+  for (int used = 1; used <= n; ++used) {
+    ++fill;
+    if (fill * 5 >= mask * 3) {
+      const size_t minused = used > 50000 ? (size_t)used * 2 : (size_t)used * 4;
+      size_t ns = 8;
+      while (ns <= minused) ns <<= 1;
+      best = std::max(best, ns + mask + 1);
+      mask = ns - 1;
+    }
+  }
+  return (int)best;
+}
+
+extern "C" int qldpc_osd_device(const qldpc_code* code, int64_t count, const uint8_t* d_syn,
+                                const int32_t* d_perm, int order, uint8_t* d_ehat, int32_t* d_status,
+                                void* stream) {
+  if (!code) return fail(QLDPC_EINVAL, "code is null");
+  if (count < 0) return fail(QLDPC_EINVAL, "negative count");
+  if (count == 0) return QLDPC_OK;
+  if (code->device < 0) return fail(QLDPC_EHIP, "no HIP device was visible when the code was created");
+  if (!d_syn || !d_perm || !d_ehat || !d_status) return fail(QLDPC_EINVAL, "null device buffer");
+  const int m = code->m, n = code->n;
+  if (m > 1024) return fail(QLDPC_EUNSUP, "GPU OSD supports m <= 1024 rows (got %d)", m);
+  const int nw = qldpc::osd_nw_of((n + 1 + 63) / 64);
+  const void* k = qldpc::select_osd_kernel(nw);
+  if (!k) return fail(QLDPC_EUNSUP, "GPU OSD supports n <= 2111 columns (got %d)", n);
+  int lds = 4 * n + 4 * (m + 2) + n;
+  lds = align16(lds) + 8 * 3 * nw + 4 * 32 + 16;
+  if (order == 1) lds += 4 * setdiff_table_ints(n);
+  int dev = 0, max_lds = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  HIP_TRY(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
+  if (lds > max_lds) return fail(QLDPC_EUNSUP, "GPU OSD needs %d B LDS", lds);
+  HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds));
+  qldpc::OsdArgs a{};
+  a.row_ptr = code->d_row_ptr;
+  a.col_idx = code->d_col_idx;
+  a.perm = d_perm;
+  a.syn = d_syn;
+  a.ehat = d_ehat;
+  a.status = d_status;
+  a.m = m;
+  a.n = n;
+  a.rank = code->rank;
+  a.order = order;
+  const int block = std::max(64, (m + 63) / 64 * 64);
+  int64_t done = 0;
+  while (done < count) {  // grid.x limit
+    const int64_t g = std::min<int64_t>(count - done, 1 << 30);
+    qldpc::OsdArgs ai = a;
+    ai.perm = d_perm + done * n;
+    ai.syn = d_syn + done * m;
+    ai.ehat = d_ehat + done * n;
+    ai.status = d_status + done;
+    void* params[] = {(void*)&ai};
+    HIP_TRY(hipLaunchKernel(k, dim3((unsigned)g), dim3(block), params, (size_t)lds, (hipStream_t)stream));
+    done += g;
+  }
+  return QLDPC_OK;
 }

@@ -1,0 +1,253 @@
+// osd_kernels.hip — batched OSD post-decoding on MI355X (gfx950).
+//
+// Replaces OSDdec (qLDPCsim/decoders.py:299-370) with its gf2math.rank /
+// gf2math.REF calls (gf2math.py:91-187) for a batch of non-converged shots.
+// One workgroup = one shot; thread t owns row t of the column-permuted matrix
+// Hp = H[:, perm] (perm = the reliability order, computed by the caller with
+// NumPy exactly as decoders.py:320-325), held bit-packed in VGPRs, with the
+// syndrome as an augmented column.
+//
+// Equivalences used (OSD):
+//  * Gaussian elimination over the columns of Hp in order, pivot = first row at
+//    or below the current pivot row holding a 1 (gf2math.REF's rule), finds a
+//    pivot exactly in the columns that raise the rank — the greedy
+//    complementary information set J of decoders.py:329-342 (plus column 0,
+//    which the reference takes unconditionally).
+//  * Non-pivot columns cause no row operation, so the row operations equal
+//    those of REF(Hp[:, J], reduced=True); applied to the augmented syndrome
+//    they give T @ s. With R = T @ Hp: T @ sJ = T @ s + R[:, I] @ e_I (mod 2),
+//    so e_J = (T @ sJ)[:|J|] (decoders.py:352-358) needs one elimination.
+//  * Order semantics with the reference's aliasing: order 1
+//    flips e_perm[infoSet[0]] (CPython set order, emulated), order >= 2 is
+//    order 0.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "osd_kernels.h"
+
+namespace qldpc {
+
+__device__ int first_setdiff(int n, const unsigned char* inJ, int nJ, int* table);
+
+template <int NW>
+__global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
+  // LDS: inv_perm[n] | J list [m+1] | inJ bytes [n] | emask [NW] u64 |
+  //      pivot row [NW] | swap row [NW] | wave slots [2][16] | set table
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int m = a.m, n = a.n;
+  int* inv = (int*)lds;
+  int* Jl = inv + n;
+  unsigned char* inJ = (unsigned char*)(Jl + m + 2);
+  uint64_t* emask = (uint64_t*)(((uintptr_t)(inJ + n) + 15) & ~(uintptr_t)15);
+  uint64_t* pivbuf = emask + NW;
+  uint64_t* swapbuf = pivbuf + NW;
+  int* slots = (int*)(swapbuf + NW);               // [2][16]
+  int* misc = slots + 32;                          // [0]=|J| [1]=status [2]=first info index
+  int* table = misc + 4;                           // CPython set emulation (order 1)
+
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6, nwaves = blockDim.x >> 6;
+  const long long shot = blockIdx.x;
+  const int32_t* perm = a.perm + shot * (long long)n;
+  const uint8_t* syn = a.syn + shot * (long long)m;
+  uint8_t* ehat = a.ehat + shot * (long long)n;
+
+  for (int i = t; i < n; i += blockDim.x) {
+    inv[perm[i]] = i;
+    inJ[i] = 0;
+  }
+  __syncthreads();
+
+  // my row of Hp (+ syndrome bit at column n)
+  uint64_t R[NW];
+#pragma unroll
+  for (int w = 0; w < NW; ++w) R[w] = 0;
+  const bool own = t < m;
+  if (own) {
+    for (int e = a.row_ptr[t]; e < a.row_ptr[t + 1]; ++e) {
+      const int i = inv[a.col_idx[e]];
+#pragma unroll
+      for (int w = 0; w < NW; ++w)
+        if ((i >> 6) == w) R[w] |= 1ull << (i & 63);
+    }
+    if (syn[t] & 1) {
+#pragma unroll
+      for (int w = 0; w < NW; ++w)
+        if ((n >> 6) == w) R[w] |= 1ull << (n & 63);
+    }
+  }
+
+  int xrow = 0, rank = 0, nJ = 0, step = 0;
+  bool done = a.rank == 0;                          // rank(H) = 0: IndexError below
+  if (t == 0) {
+    Jl[0] = 0;                                      // column 0 always (decoders.py:329)
+    inJ[0] = 1;
+  }
+  nJ = 1;
+  for (int w = 0; w < NW; ++w) {
+    if (done || 64 * w >= n) break;
+    for (int b = 0; b < 64; ++b) {
+      const int i = 64 * w + b;
+      if (i >= n || done) break;
+      uint64_t cur = 0;                             // R[w] without a runtime register index
+#pragma unroll
+      for (int q = 0; q < NW; ++q) cur = (q == w) ? R[q] : cur;
+      const bool has = own && ((cur >> b) & 1ull);
+      const uint64_t bal = __ballot(has && t >= xrow);
+      int* sl = slots + 16 * (step & 1);
+      if (lane == 0) sl[wave] = bal ? wave * 64 + __builtin_ctzll(bal) : 0x7fffffff;
+      __syncthreads();
+      int piv = 0x7fffffff;
+      for (int q = 0; q < nwaves; ++q) piv = min(piv, sl[q]);
+      ++step;
+      if (piv == 0x7fffffff) continue;              // dependent column: not in J
+      // pivot row `piv` moves to position xrow (REF's row swap), then every
+      // other row holding a 1 in column i is XOR-ed with it (below and above)
+      if (t == piv) {
+#pragma unroll
+        for (int q = 0; q < NW; ++q) pivbuf[q] = R[q];
+      }
+      if (t == xrow && piv != xrow) {
+#pragma unroll
+        for (int q = 0; q < NW; ++q) swapbuf[q] = R[q];
+      }
+      __syncthreads();
+      if (t == piv && piv != xrow) {
+#pragma unroll
+        for (int q = 0; q < NW; ++q) R[q] = swapbuf[q];   // old row xrow: 0 in column i
+      } else if (t == xrow) {
+#pragma unroll
+        for (int q = 0; q < NW; ++q) R[q] = pivbuf[q];
+      } else if (has) {
+#pragma unroll
+        for (int q = 0; q < NW; ++q)
+          if (q >= w) R[q] ^= pivbuf[q];                 // pivot row is 0 left of column i
+      }
+      if (i != 0) {
+        if (t == 0) {
+          Jl[nJ] = i;
+          inJ[i] = 1;
+        }
+        ++nJ;
+      }
+      ++xrow;
+      ++rank;
+      if (rank >= a.rank || xrow >= m) done = true;
+      if (i == 0 && done) rank = -1;                // column 0 alone reaches rank(H): the
+    }                                               // greedy loop never breaks (:333-342)
+  }
+  if (rank < a.rank) {                              // greedy loop runs past column n-1
+    if (t == 0) a.status[shot] = 1;                 // (the reference raises IndexError)
+    return;
+  }
+  __syncthreads();
+  // information-set values e_I (e_perm = e_hat[perm], decoders.py:345)
+  for (int w = t; w < NW; w += blockDim.x) {
+    uint64_t bits = 0;
+    for (int b = 0; b < 64; ++b) {
+      const int i = 64 * w + b;
+      if (i < n && !inJ[i] && (ehat[perm[i]] & 1)) bits |= 1ull << b;
+    }
+    emask[w] = bits;
+  }
+  if (t == 0) {
+    int i0 = -1;
+    if (a.order == 1 && nJ < n) {
+      // first element of CPython's set(range(n)) - set(J) (decoders.py:344)
+      i0 = first_setdiff(n, inJ, nJ, table);
+    }
+    misc[2] = i0;
+  }
+  __syncthreads();
+  const int i0 = misc[2];
+  if (t == 0 && i0 >= 0) emask[i0 >> 6] ^= 1ull << (i0 & 63);  // order-1 flip (:349-350)
+  __syncthreads();
+  // e_J = (T sJ)[:|J|], T sJ = T s + R[:, I] e_I (mod 2)   (decoders.py:352-358)
+  if (own && t < nJ) {
+    uint64_t acc = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      if (w == (n >> 6)) acc ^= (R[w] >> (n & 63)) & 1ull;      // T s (augmented column)
+      acc ^= (uint64_t)(__builtin_popcountll(R[w] & emask[w]) & 1);
+    }
+    ehat[perm[Jl[t]]] = (uint8_t)(acc & 1ull);                // e_hat[perm] = ... (:368)
+  }
+  if (t == 0 && i0 >= 0) ehat[perm[i0]] ^= 1;
+  if (t == 0) a.status[shot] = 0;
+}
+
+// CPython setobject.c emulation (set_difference -> set_add_entry with
+// resize; LINEAR_PROBES 9, PERTURB_SHIFT 5) for small-int keys, one thread.
+__device__ int first_setdiff(int n, const unsigned char* inJ, int nJ, int* table) {
+  if ((n >> 2) > nJ) {
+    for (int i = 0; i < n; ++i)
+      if (!inJ[i]) return i;
+    return -1;
+  }
+  unsigned mask = 7, fill = 0, used = 0;
+  for (unsigned s = 0; s <= mask; ++s) table[s] = -1;
+  for (int key = 0; key < n; ++key) {
+    if (inJ[key]) continue;
+    unsigned perturb = (unsigned)key, i = (unsigned)key & mask;
+    while (true) {
+      unsigned probes = (i + 9 <= mask) ? 9 : 0, k = i;
+      bool placed = false;
+      while (true) {
+        if (table[k] < 0) { table[k] = key; placed = true; break; }
+        if (probes-- == 0) break;
+        ++k;
+      }
+      if (placed) break;
+      perturb >>= 5;
+      i = (i * 5 + 1 + perturb) & mask;
+    }
+    ++fill;
+    ++used;
+    if (fill * 5 >= mask * 3) {
+      const unsigned minused = used > 50000 ? used * 2 : used * 4;
+      unsigned newsize = 8;
+      while (newsize <= minused) newsize <<= 1;
+      // re-insert (old table order) into the new one: copy old entries to the
+      // upper half of the scratch first (newsize > 2*(mask+1) always here)
+      int* old = table + newsize;
+      for (unsigned s = 0; s <= mask; ++s) old[s] = table[s];
+      for (unsigned s = 0; s < newsize; ++s) table[s] = -1;
+      const unsigned nmask = newsize - 1;
+      for (unsigned s = 0; s <= mask; ++s) {
+        const int kk = old[s];
+        if (kk < 0) continue;
+        unsigned pt = (unsigned)kk, j = (unsigned)kk & nmask;
+        while (true) {
+          if (table[j] < 0) { table[j] = kk; break; }
+          bool ok = false;
+          if (j + 9 <= nmask) {
+            for (int q = 0; q < 9; ++q) {
+              ++j;
+              if (table[j] < 0) { table[j] = kk; ok = true; break; }
+            }
+          }
+          if (ok) break;
+          pt >>= 5;
+          j = (j * 5 + 1 + pt) & nmask;
+        }
+      }
+      mask = nmask;
+    }
+  }
+  for (unsigned s = 0; s <= mask; ++s)
+    if (table[s] >= 0) return table[s];
+  return -1;
+}
+
+const void* select_osd_kernel(int nw) {
+  if (nw <= 4) return (const void*)&osd_kernel<4>;
+  if (nw <= 9) return (const void*)&osd_kernel<9>;
+  if (nw <= 17) return (const void*)&osd_kernel<17>;
+  if (nw <= 33) return (const void*)&osd_kernel<33>;
+  return nullptr;
+}
+
+int osd_nw_of(int nw) { return nw <= 4 ? 4 : nw <= 9 ? 9 : nw <= 17 ? 17 : nw <= 33 ? 33 : 0; }
+
+}  // namespace qldpc

@@ -32,7 +32,7 @@ from . import _lib
 from .schedule import pack_layers
 
 __all__ = ["MS_decoder", "BP_decoder", "OSDdec", "decode_batch", "DecodeResult", "osd_perm",
-           "apply_osd"]
+           "osd_perms", "apply_osd", "apply_osd_device"]
 
 
 @dataclass
@@ -121,6 +121,57 @@ def osd_perm(posteriorLLRs):
     return np.argsort(reliability)
 
 
+def osd_perms(post, nthreads=None):
+    """Row-wise reliability orders (decoders.py:320-325) of a [k, n] posterior
+    block: NumPy's own exp / argsort, chunked over host threads (identical to
+    per-row calls; NumPy releases the GIL in these loops)."""
+    post = np.asarray(post)
+    if post.shape[0] == 0:
+        return np.zeros((0, post.shape[1]), np.int32)
+
+    def one(P):
+        sat = np.where(np.abs(P) < 100.0, P, 100.0 * np.sign(P))
+        prob = 1. / (1. + np.exp(sat))
+        rel = np.where(prob > 0.5, prob, 1 - prob)
+        return np.argsort(rel, axis=1).astype(np.int32)
+
+    import os
+    nthreads = nthreads or min(16, os.cpu_count() or 1)
+    if post.shape[0] < 256 or nthreads <= 1:
+        return one(post)
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(nthreads) as ex:
+        return np.concatenate(list(ex.map(one, np.array_split(post, 4 * nthreads))))
+
+
+def apply_osd_device(H, syn, res, order, stream=None):
+    """GPU OSD (qldpc_osd_device) for the non-converged shots of a device
+    decode `res` (DecodeResult of torch tensors, with posteriors): only their
+    posteriors travel to the host for NumPy's reliability order; the GF(2)
+    work runs on the GPU. Updates res.ehat in place."""
+    import torch
+    if res.post is None:
+        raise ValueError("apply_osd_device needs the decode's posteriors (want_post=True)")
+    bad = ((res.flags & _lib.FLAG_CONVERGED) == 0).nonzero().flatten()
+    k = int(bad.numel())
+    if k == 0:
+        return res.ehat
+    dev = res.ehat.device
+    code = _lib.code_for(H, dev.index)
+    perms = torch.as_tensor(osd_perms(res.post[bad].cpu().numpy()), device=dev)
+    syn_b = syn[bad].contiguous()
+    e_b = res.ehat[bad].contiguous()
+    status = torch.empty(k, dtype=torch.int32, device=dev)
+    st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    _lib.check(_lib.lib.qldpc_osd_device(code.handle, k, syn_b.data_ptr(), perms.data_ptr(), int(order),
+                                         e_b.data_ptr(), status.data_ptr(), st))
+    if bool((status != 0).any()):
+        # the reference's greedy basis loop indexes past column n-1 (decoders.py:333-342)
+        raise IndexError("OSD: column basis search ran past the last column")
+    res.ehat[bad] = e_b
+    return res.ehat
+
+
 def apply_osd(H, syn, ehat, post, flags, order, nthreads=0):
     """OSD post-step for every non-converged row (decoders.py:179-180, :287-288).
 
@@ -130,7 +181,7 @@ def apply_osd(H, syn, ehat, post, flags, order, nthreads=0):
     if idx.size == 0:
         return ehat
     code = _lib.code_for(H)
-    perms = np.ascontiguousarray(np.stack([osd_perm(post[i]) for i in idx]), dtype=np.int32)
+    perms = np.ascontiguousarray(osd_perms(post[idx]), dtype=np.int32)
     sub_syn = np.ascontiguousarray(syn[idx], dtype=np.uint8)
     sub_e = np.ascontiguousarray(ehat[idx], dtype=np.uint8)
     _lib.check(_lib.lib.qldpc_osd_decode_batch(code.handle, idx.size, _lib.ptr(sub_syn),

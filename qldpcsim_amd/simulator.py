@@ -153,22 +153,6 @@ class DeviceChannel:
         return dict(zip(COUNTER_KEYS, (int(x) for x in v)))
 
 
-def _osd_on_device_result(H, syn_d, r, order):
-    """OSD post-step (decoders.py:179-180) for the non-converged shots of a
-    device decode: only those rows travel to the host."""
-    import torch
-    from . import _lib
-    bad = ((r.flags & _lib.FLAG_CONVERGED) == 0).nonzero().flatten()
-    if bad.numel() == 0:
-        return
-    syn = syn_d[bad].cpu().numpy()
-    e = r.ehat[bad].cpu().numpy()
-    post = r.post[bad].cpu().numpy()
-    flags = np.zeros(len(e), np.int32)
-    decoders.apply_osd(H, syn, e, post, flags, order)
-    r.ehat[bad] = torch.as_tensor(e, device=r.ehat.device)
-
-
 def _device_ok():
     try:
         import torch
@@ -241,9 +225,9 @@ def simulate_p(Hx: np.ndarray, Hz: np.ndarray, p: float, shots: int = 1000, decT
                                        layer_ptr=lpX, layer_rows=lrX)
             rZ = decoders.decode_batch(Hx, sy_x, p / 3, decIterations, algo=decType, want_post=want_post,
                                        layer_ptr=lpZ, layer_rows=lrZ)
-            if osd >= 0:
-                _osd_on_device_result(Hz, sy_z, rX, osd)
-                _osd_on_device_result(Hx, sy_x, rZ, osd)
+            if osd >= 0:                               # (decoders.py:179-180), on the GPU
+                decoders.apply_osd_device(Hz, sy_z, rX, osd)
+                decoders.apply_osd_device(Hx, sy_x, rZ, osd)
             c = ch.count(sy_z, sy_x, errX, errZ, rX.ehat, rZ.ehat, rX.iters, rZ.iters)
         elif samples is not None:
             sl = slice(my_start + done, my_start + done + B)

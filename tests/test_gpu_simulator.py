@@ -17,7 +17,7 @@ def test_simulate_p_counters_match_oracle_restatement(code, decType, sched, osd,
     from oracle import oracle
     from qldpcsim_amd import codes, schedule, simulator
     Hx, Hz = codes.load_code(code)
-    shots = 3000
+    shots = 1200
     smp = simulator.sample_channel(Hx, Hz, p, shots, np.random.default_rng(17))
     got = simulator.simulate_p(Hx, Hz, p, shots=shots, decType=decType, decIterations=30,
                                decSchedule=sched, OSDorder=osd, samples=smp, batch_size=1000,

@@ -62,6 +62,30 @@ def run(code, algo, sched, p, max_iter, B, reps=2):
             "shots_per_s_wall": reps * B / wall, "avg_iters": its / (2 * reps * B)}
 
 
+def run_osd(code, count, order=0):
+    """GPU OSD throughput on random posteriors / arbitrary syndromes."""
+    Hx, Hz = codes.load_code(code)
+    H = Hz
+    rng = np.random.default_rng(1)
+    post = rng.normal(0, 3, (count, H.shape[1]))
+    t0 = time.perf_counter()
+    perms = torch.as_tensor(decoders.osd_perms(post), device="cuda")
+    t_perm = time.perf_counter() - t0
+    syn = torch.randint(0, 2, (count, H.shape[0]), dtype=torch.uint8, device="cuda")
+    e = torch.as_tensor((post < 0).astype(np.uint8), device="cuda")
+    st = torch.empty(count, dtype=torch.int32, device="cuda")
+    code_h = _lib.code_for(H, 0)
+    for _ in range(2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        _lib.check(_lib.lib.qldpc_osd_device(code_h.handle, count, syn.data_ptr(), perms.data_ptr(), order,
+                                             e.data_ptr(), st.data_ptr(), None))
+        torch.cuda.synchronize()
+        t_gpu = time.perf_counter() - t0
+    return {"osd_code": code, "count": count, "order": order, "gpu_osd_per_s": count / t_gpu,
+            "host_perm_per_s": count / t_perm}
+
+
 def main():
     quick = "--quick" in sys.argv
     S = 1 << (16 if quick else 18)
@@ -78,6 +102,10 @@ def main():
         ("LP118_2", "MS", "F", None, 50, S),
         ("LP118_2", "BP", "L", 0.05, 100, S // 2),           # configs[4] (decoder part)
     ]
+    if "--osd" in sys.argv:
+        for c in ("LP04_0", "LP118_0", "LP118_2"):
+            print(json.dumps(run_osd(c, 8192)), flush=True)
+        return
     for pt in pts:
         print(json.dumps(run(*pt)), flush=True)
 
