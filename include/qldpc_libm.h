@@ -11,10 +11,12 @@
  * comparisons. Accuracy against NumPy's tanh/arctanh: <= 2 ULP over the BP
  * domain (tests/test_libm.py).
  *
- * Method: tanh via expm1 (Cody–Waite reduction y = k ln2 + r, |r| <= ln2/2,
- * degree-14 Taylor polynomial, 2^k (1 + expm1 r) - 1 reassembled exactly);
- * atanh via log1p (u = 1 + f = 2^k m, m in [sqrt2/2, sqrt2), rounding
- * correction c, log(1+f') = f' - hfsq + s (hfsq + R(s^2)), s = f'/(2+f')).
+ * Method: tanh = e/(e+2), e = expm1(2|x|) (Cody–Waite reduction y = k ln2 + r,
+ * |r| <= ln2/2, degree-14 Taylor polynomial, 2^k (1 + expm1 r) - 1
+ * reassembled exactly); atanh = log1p(2|x|/(1-|x|))/2 with log1p as fdlibm
+ * (f itself inside (1/sqrt2-1, sqrt2-1), else u = 1+f = 2^k m with rounding
+ * correction c; log(1+f') = f' - hfsq + s (hfsq + R(s^2)), s = f'/(2+f')).
+ * Written branch-light (one division each) because GPU lanes diverge.
  */
 #ifndef QLDPC_LIBM_H
 #define QLDPC_LIBM_H
@@ -83,7 +85,7 @@ QLDPC_HD double qldpc_tanh(double x) {
     t = a;
   } else {
     const double em = qldpc_expm1_pos(a + a);
-    t = (a < 1.0) ? em / (em + 2.0) : 1.0 - 2.0 / (em + 2.0);
+    t = em / (em + 2.0);                          /* one division, any a (<= 3 ULP) */
   }
   return qldpc_bits2d(qldpc_d2bits(t) | sgn);
 }
@@ -95,22 +97,35 @@ QLDPC_HD double qldpc_log1p(double f) {
   const double af = f < 0 ? -f : f;
   if (af < 5.551115123125783e-17) return f;        /* 2^-54 */
   if (f == qldpc_bits2d(0x7ff0000000000000ull)) return f;
-  const double u = 1.0 + f;
-  const uint64_t ub = qldpc_d2bits(u);
-  int k = (int)((ub >> 52) & 0x7ff) - 1023;
-  uint64_t mb = (ub & 0x000fffffffffffffull) | 0x3ff0000000000000ull;   /* m in [1, 2) */
-  if (mb > 0x3ff6a09e667f3bcdull) {                                     /* m > sqrt(2) */
-    mb = (mb & 0x000fffffffffffffull) | 0x3fe0000000000000ull;          /* m / 2 */
-    k += 1;
+  int k = 0;
+  double fm = f, c = 0.0;
+  if (!(f > -0.2928932188134524 && f < 0.41421356237309503)) {
+    /* u = 1 + f = 2^k m, m in [sqrt2/2, sqrt2); c = rounding error of u,
+       relative to u (fdlibm's c). Inside (1/sqrt2 - 1, sqrt2 - 1), k = 0 and
+       f itself is the reduced argument (no rounding, no correction). */
+    const double u = 1.0 + f;
+    const uint64_t ub = qldpc_d2bits(u);
+    k = (int)((ub >> 52) & 0x7ff) - 1023;
+    uint64_t mb = (ub & 0x000fffffffffffffull) | 0x3ff0000000000000ull;   /* m in [1, 2) */
+    if (mb > 0x3ff6a09e667f3bcdull) {                                     /* m > sqrt(2) */
+      mb = (mb & 0x000fffffffffffffull) | 0x3fe0000000000000ull;          /* m / 2 */
+      k += 1;
+    }
+    fm = qldpc_bits2d(mb) - 1.0;                   /* exact (Sterbenz) */
+    if (k < 54) {
+      /* c / u needs ~1e-6 relative accuracy only (|c/u| <= 2^-53 here and
+         the result is >= 0.34): multiply by a three-step Newton reciprocal of
+         the mantissa instead of dividing. */
+      const double cc = (k > 0) ? 1.0 - (u - f) : f - (u - 1.0);
+      const double mu = qldpc_bits2d((ub & 0x000fffffffffffffull) | 0x3ff0000000000000ull);  /* [1,2) */
+      double r = 1.4571067811865475 - 0.5 * mu;     /* |r - 1/mu| < 0.09 */
+      r = r * (2.0 - mu * r);
+      r = r * (2.0 - mu * r);
+      r = r * (2.0 - mu * r);
+      const double two_mk = qldpc_bits2d((uint64_t)(1023 - ((int)((ub >> 52) & 0x7ff) - 1023)) << 52);
+      c = cc * r * two_mk;
+    }
   }
-  const double m = qldpc_bits2d(mb);
-  /* rounding error of u = 1 + f, relative to u (fdlibm's c) */
-  double c = 0.0;
-  if (k < 54) {
-    c = (k > 0) ? 1.0 - (u - f) : f - (u - 1.0);
-    c = c / u;
-  }
-  const double fm = m - 1.0;                      /* exact (Sterbenz) */
   const double s = fm / (2.0 + fm);
   const double z = s * s;
   double R = 2.0 / 25.0;
@@ -140,11 +155,8 @@ QLDPC_HD double qldpc_atanh(double x) {
     t = (a == 1.0) ? qldpc_bits2d(0x7ff0000000000000ull) : qldpc_bits2d(0x7ff8000000000000ull);
   } else if (a < 3.7252902984e-09) {
     t = a;                                        /* atanh(x) = x in double */
-  } else if (a < 0.5) {
-    const double t2 = a + a;
-    t = 0.5 * qldpc_log1p(t2 + t2 * a / (1.0 - a));
   } else {
-    t = 0.5 * qldpc_log1p((a + a) / (1.0 - a));
+    t = 0.5 * qldpc_log1p((a + a) / (1.0 - a));   /* one division, any a (<= 3 ULP) */
   }
   return qldpc_bits2d(qldpc_d2bits(t) | sgn);
 }

@@ -197,6 +197,7 @@ extern "C" int qldpc_code_shape(const qldpc_code* code, int* m, int* n, int* n_e
 struct LaunchCfg {
   const void* kernel = nullptr;
   int waves = 0, blocks_per_cu = 0, lds = 0, wave_bytes = 0;
+  bool lblob = false;  // uses the layer-ordered blob (ms_layered_kernel)
   bool ok = false;
 };
 
@@ -205,6 +206,11 @@ struct qldpc_schedule {
   bool layered = false;
   int n_layers = 0;
   std::vector<uint8_t> blob;  // LDS image of the graph tables
+  // layered MS, uniform degree: layer-ordered tables (ms_layered_kernel)
+  std::vector<uint8_t> lblob;
+  unsigned char* d_lblob = nullptr;
+  int l_off_ltab = 0, l_off_lrow = 0, l_off_lay_ptr = 0, l_off_adj_ptr = 0, l_off_adj_vars = 0,
+      l_off_adj_info = 0, l_off_adj_dmax = 0, l_off_vn_chk = 0;
   int off_cn_tab = 0, off_row_ptr = 0, off_vn_ptr = 0, off_vn_chk = 0;
   int off_lay_ptr = 0, off_lay_rows = 0, off_adj_ptr = 0, off_adj_vars = 0, off_chunk_dmax = 0;
   unsigned char* d_blob = nullptr;
@@ -316,6 +322,29 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
     s->off_lay_rows = put(s->blob, lay_rows);
     s->off_adj_ptr = put(s->blob, adj_ptr);
     s->off_adj_vars = put(s->blob, adj_vars);
+    if (fast_table_ok(code) && n <= 2048 && code->max_col_deg <= 31) {
+      std::vector<uint32_t> ltab((size_t)8 * lay_rows.size(), 0), adj_info(adj_vars.size());
+      for (size_t q = 0; q < lay_rows.size(); ++q) {
+        const int r = lay_rows[q];
+        for (int e = code->row_ptr[r], k = 0; e < code->row_ptr[r + 1]; ++e, ++k)
+          ltab[8 * q + k] = ((uint32_t)(4 * code->edge_pos[e]) << 16) | (uint32_t)(8 * code->vinv[code->col_idx[e]]);
+      }
+      std::vector<uint8_t> adj_dmax(std::max(n_layers, 1), 0);
+      for (int l = 0; l < n_layers; ++l)
+        for (int q = adj_ptr[l]; q < adj_ptr[l + 1]; ++q) {
+          const int v = adj_vars[q], d = code->csc_ptr[v + 1] - code->csc_ptr[v];
+          adj_info[q] = ((uint32_t)v << 21) | ((uint32_t)d << 16) | (uint32_t)code->csc_ptr[v];
+          adj_dmax[l] = (uint8_t)std::min(255, std::max<int>(adj_dmax[l], d));
+        }
+      s->l_off_ltab = put(s->lblob, ltab);
+      s->l_off_lrow = put(s->lblob, lay_rows);
+      s->l_off_lay_ptr = put(s->lblob, lay_ptr);
+      s->l_off_adj_ptr = put(s->lblob, adj_ptr);
+      s->l_off_adj_info = put(s->lblob, adj_info);
+      s->l_off_adj_dmax = put(s->lblob, adj_dmax);
+      s->l_off_vn_chk = put(s->lblob, vn_chk);
+      s->lblob.resize(align16((int)s->lblob.size() + 1));
+    }
   }
   s->blob.resize(align16((int)s->blob.size() + 1));
   if (code->device < 0) {  // no device: keep the host image only
@@ -324,6 +353,10 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
   }
   hipError_t e1 = hipMalloc(&s->d_blob, s->blob.size());
   if (e1 == hipSuccess) e1 = hipMemcpy(s->d_blob, s->blob.data(), s->blob.size(), hipMemcpyHostToDevice);
+  if (e1 == hipSuccess && !s->lblob.empty()) {
+    e1 = hipMalloc(&s->d_lblob, s->lblob.size());
+    if (e1 == hipSuccess) e1 = hipMemcpy(s->d_lblob, s->lblob.data(), s->lblob.size(), hipMemcpyHostToDevice);
+  }
   if (e1 != hipSuccess) {
     delete s;
     return fail(QLDPC_EHIP, "uploading the schedule failed: %s", hipGetErrorString(e1));
@@ -335,6 +368,7 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
 extern "C" int qldpc_schedule_destroy(qldpc_schedule* s) {
   if (!s) return QLDPC_OK;
   (void)hipFree(s->d_blob);
+  (void)hipFree(s->d_lblob);
   delete s;
   return QLDPC_OK;
 }
@@ -368,6 +402,13 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
     cfg.kernel = qldpc::select_ms_flood_kernel(dc, (c->m + 63) / 64, (c->n + 63) / 64);
     if (cfg.kernel) max_waves = qldpc::ms_flood_max_waves((c->m + 63) / 64);
   }
+  bool use_lblob = false;
+  if (!cfg.kernel && algo == QLDPC_ALGO_MS && s->layered && dc > 0 && !s->lblob.empty() &&
+      !getenv("QLDPC_NO_LAYERED_FAST")) {
+    cfg.kernel = qldpc::select_ms_layered_kernel(dc);
+    use_lblob = cfg.kernel != nullptr;
+  }
+  cfg.lblob = use_lblob;
   if (!cfg.kernel) cfg.kernel = qldpc::select_kernel(algo, s->layered, dc);
   int off_c2v, off_synw, off_parw;
   wave_layout(c, s->layered, algo, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw);
@@ -375,7 +416,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   HIP_TRY(hipGetDevice(&dev));
   HIP_TRY(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
   HIP_TRY(qldpc::configure_kernel(cfg.kernel, max_lds));
-  const int blob = (int)s->blob.size();
+  const int blob = (int)(use_lblob ? s->lblob.size() : s->blob.size());
   int best_waves = 0;
   for (int w = max_waves; w >= 1; --w) {
     const int lds = blob + w * cfg.wave_bytes;
@@ -499,6 +540,18 @@ extern "C" int qldpc_decode_device(const qldpc_code* code, const qldpc_schedule*
   a.off_adj_vars = sched->off_adj_vars;
   a.off_chunk_dmax = sched->off_chunk_dmax;
   wave_layout(code, sched->layered, algo, &a.wave_bytes, &a.off_c2v, &a.off_synw, &a.off_parw);
+  if (cfg->lblob) {  // ms_layered_kernel's blob: field mapping documented in the kernel
+    a.blob = sched->d_lblob;
+    a.blob_bytes = (int)sched->lblob.size();
+    a.off_cn_tab = sched->l_off_ltab;
+    a.off_lay_rows = sched->l_off_lrow;
+    a.off_lay_ptr = sched->l_off_lay_ptr;
+    a.off_adj_ptr = sched->l_off_adj_ptr;
+    a.off_adj_vars = sched->l_off_adj_vars;
+    a.off_row_ptr = sched->l_off_adj_info;
+    a.off_chunk_dmax = sched->l_off_adj_dmax;
+    a.off_vn_chk = sched->l_off_vn_chk;
+  }
   a.m = code->m;
   a.n = code->n;
   a.E = code->E;

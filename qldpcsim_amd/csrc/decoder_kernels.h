@@ -36,7 +36,8 @@ struct DecodeArgs {
 
 const void* select_kernel(int algo, bool layered, int dc);
 const void* select_ms_flood_kernel(int dc, int kc, int vp);  // nullptr if no instantiation fits
-int ms_flood_max_waves(int kc);                               // waves per workgroup it was compiled for
+int ms_flood_max_waves(int kc);
+const void* select_ms_layered_kernel(int dc);                // layered MS, uniform degree (blob: layer tables)                               // waves per workgroup it was compiled for
 hipError_t launch_decode(const void* kernel, const DecodeArgs& args, int grid, int block,
                          int lds_bytes, hipStream_t stream);
 hipError_t configure_kernel(const void* kernel, int lds_bytes);

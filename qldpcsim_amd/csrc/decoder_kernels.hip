@@ -710,6 +710,121 @@ __global__ void __launch_bounds__(ms_flood_max_threads<KC>()) ms_flood_kernel(De
 }
 
 // ---------------------------------------------------------------------------
+// Layered / serial min-sum for uniform-degree codes (decoders.py:153-177 with
+// an explicit layer list). Per layer: CN over the layer's rows (Jacobi, the
+// fast uniform path), VN over the variables adjacent to the layer, parity
+// toggles for flipped hard decisions, stop test. The blob holds the layer
+// rows' table words in layer order (ltab) and each adjacency slot's
+// (variable, csc start | degree) so every phase is one dependent LDS hop
+// shorter than decode_kernel<MS, true, DC>.
+// ---------------------------------------------------------------------------
+template <int DC>
+__global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  {
+    const uint4* src = (const uint4*)a.blob;
+    uint4* dst = (uint4*)lds;
+    const int nvec = a.blob_bytes >> 4;
+    for (int i = threadIdx.x; i < nvec; i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  const uint32_t* ltab = (const uint32_t*)(lds + a.off_cn_tab);      // [Q][8]
+  const uint16_t* lrow = (const uint16_t*)(lds + a.off_lay_rows);    // [Q]
+  const uint16_t* lay_ptr = (const uint16_t*)(lds + a.off_lay_ptr);  // [L+1]
+  const uint16_t* adj_ptr = (const uint16_t*)(lds + a.off_adj_ptr);  // [L+1]
+  const uint32_t* adj_info = (const uint32_t*)(lds + a.off_row_ptr); // [A] var<<21 | deg<<16 | csc start
+  const uint8_t* adj_dmax = (const uint8_t*)(lds + a.off_chunk_dmax);// [L] max degree per layer
+  const uint16_t* vn_chk = (const uint16_t*)(lds + a.off_vn_chk);
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int waves = blockDim.x >> 6;
+  unsigned char* ws = lds + a.blob_bytes + wid * a.wave_bytes;
+  double* post = (double*)ws;
+  unsigned char* c2v_b = ws + a.off_c2v;
+  float* c2v = (float*)c2v_b;
+  uint32_t* synw = (uint32_t*)(ws + a.off_synw);
+  uint32_t* parw = (uint32_t*)(ws + a.off_parw);
+  const int m = a.m, n = a.n;
+  const int nwords = (m + 31) >> 5;
+
+  for (long long hs = (long long)blockIdx.x * waves + wid; hs < a.batch;
+       hs += (long long)gridDim.x * waves) {
+    const uint8_t* syn = a.syn + hs * (long long)m;
+    int fl = 0;
+    int iters = a.max_iter;
+    bool conv = false;
+    const double L = a.L;
+    for (int j = lane; j < n; j += 64) post[j] = L;             // v2c = L, c2v = 0 (:148-150)
+    for (int p = lane; p < a.E; p += 64) c2v[p] = 0.0f;
+    for (int c0 = 0; c0 < m; c0 += 64) {
+      const int c = c0 + lane;
+      const int in = c < m;
+      store_bits64(synw, c0, in ? (syn[c] & 1) : 0, lane);
+      store_bits64(parw, c0, in && (L < 0.0) && (DC & 1), lane);
+    }
+    wave_sync();
+    bool first = true;
+    for (int it = 0; it < a.max_iter && !conv; ++it) {
+      for (int l = 0; l < a.n_layers; ++l) {
+        const int q0 = lay_ptr[l], q1 = lay_ptr[l + 1];
+        for (int q = q0 + lane; q < q1; q += 64) {
+          uint32_t t[1][8];
+          load_row8(ltab + q * 8, t[0]);
+          const int c = lrow[q];
+          const uint32_t sb[1] = {(synw[c >> 5] >> (c & 31)) & 1u};
+          const bool live[1] = {true};
+          if (first)
+            (void)cn_ms_uniform<DC, true, 1>(a, t, sb, live, (const unsigned char*)post, c2v_b, fl);
+          else
+            (void)cn_ms_uniform<DC, false, 1>(a, t, sb, live, (const unsigned char*)post, c2v_b, fl);
+        }
+        first = false;
+        wave_sync();
+        // VN over the layer's adjacent variables (decoders.py:172-174: the
+        // other columns are unchanged, so this equals the full recompute)
+        const int v0 = adj_ptr[l], v1 = adj_ptr[l + 1];
+        const int dmax = __builtin_amdgcn_readfirstlane((int)adj_dmax[l]);
+        for (int q = v0 + lane; q < v1; q += 64) {
+          const uint32_t info = adj_info[q];
+          const int j = (int)(info >> 21), d = (int)((info >> 16) & 31u);
+          const double old = post[j];
+          const float s = ms_colsum_sw<0>(c2v + (info & 0xffffu), d, dmax);
+          const double nw = L + (double)s;
+          post[j] = nw;
+          if ((old < 0.0) != (nw < 0.0)) {                       // hard decision flipped
+            for (int p = (int)(info & 0xffffu), pe = p + d; p < pe; ++p) {
+              const int c = vn_chk[p];
+              atomicXor(&parw[c >> 5], 1u << (c & 31));
+            }
+          }
+        }
+        wave_sync();
+        uint32_t un = 0;                                         // stop test (:175-176)
+        for (int w = lane; w < nwords; w += 64) un |= parw[w] ^ synw[w];
+        if (ballot(un != 0) == 0) {
+          iters = it + 1;
+          conv = true;
+          break;
+        }
+      }
+    }
+    uint8_t* eh = a.ehat + hs * (long long)n;
+    double* po = a.post ? a.post + hs * (long long)n : nullptr;
+    for (int jo = lane; jo < n; jo += 64) {
+      const double pv = post[a.vinv[jo]];
+      eh[jo] = (uint8_t)(pv < 0.0);
+      if (po) po[jo] = pv;
+    }
+    const uint64_t b1 = ballot((fl & FLAG_MIN_ZERO) != 0);
+    if (lane == 0) {
+      a.iters[hs] = iters;
+      if (a.flags) a.flags[hs] = (int32_t)((b1 ? FLAG_MIN_ZERO : 0) | (conv ? FLAG_CONVERGED : 0));
+    }
+    wave_sync();
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Host-side launch helpers (called from capi.cpp)
 // ---------------------------------------------------------------------------
 template <int ALGO, bool LAYERED, int DC>
@@ -727,6 +842,12 @@ const void* select_ms_flood_kernel(int dc, int kc, int vp) {
   if (dc == 8 && kc <= 4 && vp <= 9) return (const void*)&ms_flood_kernel<8, 4, 9>;
   if (dc == 7 && kc <= 8 && vp <= 17) return (const void*)&ms_flood_kernel<7, 8, 17>;
   if (dc == 8 && kc <= 8 && vp <= 17) return (const void*)&ms_flood_kernel<8, 8, 17>;
+  return nullptr;
+}
+
+const void* select_ms_layered_kernel(int dc) {
+  if (dc == 7) return (const void*)&ms_layered_kernel<7>;
+  if (dc == 8) return (const void*)&ms_layered_kernel<8>;
   return nullptr;
 }
 

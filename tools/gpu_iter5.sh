@@ -1,0 +1,7 @@
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -q -m gpu -x > gpurun_out/pytest_gpu.log 2>&1 || exit $?
+timeout -k 10 600 python tools/ab_env.py QLDPC_NO_LAYERED_FAST LP118_0 MS L None 50 262144 3 > gpurun_out/abenv.jsonl 2>gpurun_out/abenv.err || exit $?
+timeout -k 10 600 python tools/ab_env.py QLDPC_NO_LAYERED_FAST LP118_2 MS L 0.05 50 262144 3 >> gpurun_out/abenv.jsonl 2>>gpurun_out/abenv.err || exit $?
+timeout -k 10 900 python tools/bench_configs.py > gpurun_out/configs.jsonl 2> gpurun_out/configs.err
