@@ -81,27 +81,21 @@ def decode_batch(algo, H, syn, p, max_iter, layer_ptr=None, layer_rows=None, bet
 # OSD restatement (decoders.py:299-370, gf2math.py:91-187). Small cases only.
 # --------------------------------------------------------------------------
 def gf2_rank(A):
-    """gf2math.rank (gf2math.py:91-135)."""
-    A = (np.asarray(A, dtype=np.uint8) & 1).copy()
-    m, n = A.shape
-    row = 0
-    for col in range(n):
-        piv = None
-        for r in range(row, m):
-            if A[r, col]:
-                piv = r
+    """gf2math.rank (gf2math.py:91-135): rank over GF(2), by an XOR basis of
+    the bit-packed rows (same value as the reference's row reduction)."""
+    A = np.asarray(A, dtype=np.uint8) & 1
+    basis = {}
+    r = 0
+    for row in A:
+        v = int("".join("1" if b else "0" for b in row[::-1]), 2) if row.size else 0
+        while v:
+            h = v.bit_length() - 1
+            if h not in basis:
+                basis[h] = v
+                r += 1
                 break
-        if piv is None:
-            continue
-        if piv != row:
-            A[[row, piv]] = A[[piv, row]]
-        for r in range(m):
-            if r != row and A[r, col]:
-                A[r] ^= A[row]
-        row += 1
-        if row == m:
-            break
-    return row
+            v ^= basis[h]
+    return r
 
 
 def gf2_ref_T(A):
@@ -143,17 +137,37 @@ def osd_dec(H, e_hat, syndrome, post, order=0):
     rel = np.where(prob > 0.5, prob, 1 - prob)
     perm = np.argsort(rel)
     Hp = H[:, perm]
-    J = [0]
+    # Greedy complementary info set (decoders.py:329-342). The reference calls
+    # gf2math.rank on Hp[:, J] after every append; "rank rose" is restated as
+    # "the column is independent of the kept ones" with an incremental XOR
+    # basis over bit-packed columns (same J, O(m) per column instead of a full
+    # elimination).
+    cols = [int("".join("1" if b else "0" for b in Hp[::-1, j]), 2) if Hp.shape[0] else 0
+            for j in range(Hp.shape[1])]
+    basis = {}
+
+    def insert(v):
+        while v:
+            h = v.bit_length() - 1
+            if h not in basis:
+                basis[h] = v
+                return True
+            v ^= basis[h]
+        return False
+
     max_rank = gf2_rank(Hp)
-    past = gf2_rank(Hp[:, J])
+    J = [0]
+    past = 1 if insert(cols[0]) else 0
     nxt = 1
     while True:
+        if nxt >= len(cols):
+            raise IndexError(f"index {nxt} is out of bounds for axis 1 with size {len(cols)}")
         J.append(nxt)
-        new = gf2_rank(Hp[:, J])
         nxt += 1
-        if new <= past:
+        if not insert(cols[J[-1]]):
             J.pop()
             continue
+        new = past + 1
         if new >= max_rank:
             break
         past = new

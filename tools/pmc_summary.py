@@ -1,8 +1,8 @@
 """Summarise rocprofv3 outputs for profiles/.
 
 usage: python tools/pmc_summary.py <round-tag> <code> <batch> <kernel-substr>
-  reads gpurun_out/prof_<tag>/*kernel_stats.csv, gpurun_out/pmc_fetch/*counter_collection.csv,
-  gpurun_out/pmc_write/*counter_collection.csv; writes profiles/<tag>_kernel_stats.csv and
+  reads gpurun_out/prof_<tag>/*kernel_stats.csv, gpurun_out/pmc_fetch[_<tag>]/*counter_collection.csv,
+  gpurun_out/pmc_write[_<tag>]/*counter_collection.csv; writes profiles/<tag>_kernel_stats.csv and
   profiles/<tag>_pmc.json (HBM bytes per decode launch).
 
 Counter handling (MI355X_MICROARCH.md §HBM): FETCH_SIZE and WRITE_SIZE are in
@@ -36,8 +36,11 @@ def main():
     os.makedirs(out, exist_ok=True)
     for fn in glob.glob(os.path.join(root, "gpurun_out", f"prof_{tag}", "*kernel_stats.csv")):
         shutil.copy(fn, os.path.join(out, f"{tag}_kernel_stats.csv"))
-    fetch = per_launch(os.path.join(root, "gpurun_out", "pmc_fetch", "*counter_collection.csv"), "FETCH_SIZE", kernel)
-    write = per_launch(os.path.join(root, "gpurun_out", "pmc_write", "*counter_collection.csv"), "WRITE_SIZE", kernel)
+    def pmc_dir(kind):
+        d = os.path.join(root, "gpurun_out", f"pmc_{kind}_{tag}")
+        return d if os.path.isdir(d) else os.path.join(root, "gpurun_out", f"pmc_{kind}")
+    fetch = per_launch(os.path.join(pmc_dir("fetch"), "*counter_collection.csv"), "FETCH_SIZE", kernel)
+    write = per_launch(os.path.join(pmc_dir("write"), "*counter_collection.csv"), "WRITE_SIZE", kernel)
     if not fetch or not write:
         raise SystemExit("no PMC rows for kernel " + kernel)
     f = sum(fetch) / len(fetch) * 1024 * 2
