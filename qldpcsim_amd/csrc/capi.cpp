@@ -198,6 +198,7 @@ struct LaunchCfg {
   const void* kernel = nullptr;
   int waves = 0, blocks_per_cu = 0, lds = 0, wave_bytes = 0;
   bool lblob = false;  // uses the layer-ordered blob (ms_layered_kernel)
+  bool gtab = false;     // ms_flood_kernel: global tables, LDS = wave state only
   bool ok = false;
 };
 
@@ -214,6 +215,10 @@ struct qldpc_schedule {
   int off_cn_tab = 0, off_row_ptr = 0, off_vn_ptr = 0, off_vn_chk = 0;
   int off_lay_ptr = 0, off_lay_rows = 0, off_adj_ptr = 0, off_adj_vars = 0, off_chunk_dmax = 0;
   unsigned char* d_blob = nullptr;
+  // flooding MS, uniform degree: global table image of ms_flood_kernel
+  std::vector<uint8_t> fblob;
+  unsigned char* d_fblob = nullptr;
+  int f_off_tab = 0;
   LaunchCfg cfg[2];           // per algo
   std::mutex mu;
 };
@@ -346,6 +351,43 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
       s->lblob.resize(align16((int)s->lblob.size() + 1));
     }
   }
+  if (!s->layered && fast_table_ok(code) && m <= 8 * 64) {
+    // ms_flood_kernel's global image: FloodRuns header (runs of equal column
+    // degree over the relabeled variables), then per check c = lane + 64 i the
+    // words [8c, 8c+8): (4 * csc position) << 16 | (8 * relabeled variable).
+    // Pad checks write the pad floats E..E+7 behind c2v and read post[0].
+    std::vector<int32_t> hdr(1 + 4 * QLDPC_MAX_RUNS, 0);
+    int nr = 0;
+    bool ok = true;
+    for (int j = 0; j < n;) {
+      const int d = code->csc_ptr[j + 1] - code->csc_ptr[j];
+      int e = j;
+      while (e < n && code->csc_ptr[e + 1] - code->csc_ptr[e] == d) ++e;
+      if (nr == QLDPC_MAX_RUNS) { ok = false; break; }
+      hdr[1 + nr] = j;                                   // start
+      hdr[1 + QLDPC_MAX_RUNS + nr] = e - j;              // count
+      hdr[1 + 2 * QLDPC_MAX_RUNS + nr] = d;              // degree
+      hdr[1 + 3 * QLDPC_MAX_RUNS + nr] = code->csc_ptr[j];  // csc start
+      ++nr;
+      j = e;
+    }
+    hdr[0] = nr;
+    if (ok) {
+      std::vector<uint32_t> ftab((size_t)8 * 64 * 8, 0);
+      for (int r = 0; r < 8 * 64; ++r)
+        for (int k = 0; k < 8; ++k) {
+          const int e = r < m ? code->row_ptr[r] + k : -1;
+          if (r < m && e < code->row_ptr[r + 1])
+            ftab[(size_t)8 * r + k] = ((uint32_t)(4 * code->edge_pos[e]) << 16) |
+                                      (uint32_t)(8 * code->vinv[code->col_idx[e]]);
+          else if (r >= m)
+            ftab[(size_t)8 * r + k] = (uint32_t)(4 * (code->E + k)) << 16;
+        }
+      (void)put(s->fblob, hdr);
+      s->f_off_tab = put(s->fblob, ftab);
+      s->fblob.resize(align16((int)s->fblob.size() + 1));
+    }
+  }
   s->blob.resize(align16((int)s->blob.size() + 1));
   if (code->device < 0) {  // no device: keep the host image only
     *out = s;
@@ -353,6 +395,10 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
   }
   hipError_t e1 = hipMalloc(&s->d_blob, s->blob.size());
   if (e1 == hipSuccess) e1 = hipMemcpy(s->d_blob, s->blob.data(), s->blob.size(), hipMemcpyHostToDevice);
+  if (e1 == hipSuccess && !s->fblob.empty()) {
+    e1 = hipMalloc(&s->d_fblob, s->fblob.size());
+    if (e1 == hipSuccess) e1 = hipMemcpy(s->d_fblob, s->fblob.data(), s->fblob.size(), hipMemcpyHostToDevice);
+  }
   if (e1 == hipSuccess && !s->lblob.empty()) {
     e1 = hipMalloc(&s->d_lblob, s->lblob.size());
     if (e1 == hipSuccess) e1 = hipMemcpy(s->d_lblob, s->lblob.data(), s->lblob.size(), hipMemcpyHostToDevice);
@@ -369,6 +415,7 @@ extern "C" int qldpc_schedule_destroy(qldpc_schedule* s) {
   if (!s) return QLDPC_OK;
   (void)hipFree(s->d_blob);
   (void)hipFree(s->d_lblob);
+  (void)hipFree(s->d_fblob);
   delete s;
   return QLDPC_OK;
 }
@@ -398,9 +445,11 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   const int dc = fast_table_ok(c) ? c->uniform_deg : 0;
   cfg.kernel = nullptr;
   int max_waves = QLDPC_MAX_THREADS / 64;
-  if (algo == QLDPC_ALGO_MS && !s->layered && dc > 0 && !getenv("QLDPC_NO_REGTAB")) {
-    cfg.kernel = qldpc::select_ms_flood_kernel(dc, (c->m + 63) / 64, (c->n + 63) / 64);
-    if (cfg.kernel) max_waves = qldpc::ms_flood_max_waves((c->m + 63) / 64);
+  bool gtab = false;
+  if (algo == QLDPC_ALGO_MS && !s->layered && dc > 0 && !s->fblob.empty() && !getenv("QLDPC_NO_REGTAB")) {
+    cfg.kernel = qldpc::select_ms_flood_kernel(dc, (c->m + 63) / 64);
+    gtab = cfg.kernel != nullptr;
+    if (gtab) max_waves = qldpc::ms_flood_max_waves((c->m + 63) / 64);
   }
   bool use_lblob = false;
   if (!cfg.kernel && algo == QLDPC_ALGO_MS && s->layered && dc > 0 && !s->lblob.empty() &&
@@ -409,6 +458,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
     use_lblob = cfg.kernel != nullptr;
   }
   cfg.lblob = use_lblob;
+  cfg.gtab = gtab;
   if (!cfg.kernel) cfg.kernel = qldpc::select_kernel(algo, s->layered, dc);
   int off_c2v, off_synw, off_parw;
   wave_layout(c, s->layered, algo, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw);
@@ -416,7 +466,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   HIP_TRY(hipGetDevice(&dev));
   HIP_TRY(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
   HIP_TRY(qldpc::configure_kernel(cfg.kernel, max_lds));
-  const int blob = (int)(use_lblob ? s->lblob.size() : s->blob.size());
+  const int blob = gtab ? 0 : (int)(use_lblob ? s->lblob.size() : s->blob.size());
   int best_waves = 0;
   for (int w = max_waves; w >= 1; --w) {
     const int lds = blob + w * cfg.wave_bytes;
@@ -551,6 +601,11 @@ extern "C" int qldpc_decode_device(const qldpc_code* code, const qldpc_schedule*
     a.off_row_ptr = sched->l_off_adj_info;
     a.off_chunk_dmax = sched->l_off_adj_dmax;
     a.off_vn_chk = sched->l_off_vn_chk;
+  }
+  if (cfg->gtab) {  // global tables; the LDS holds wave state only
+    a.blob = sched->d_fblob;
+    a.blob_bytes = 0;
+    a.off_cn_tab = sched->f_off_tab;
   }
   a.m = code->m;
   a.n = code->n;

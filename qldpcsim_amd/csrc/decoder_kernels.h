@@ -5,6 +5,8 @@
 
 // threads per workgroup the kernels are compiled for (waves per WG <= this/64)
 #define QLDPC_MAX_THREADS 768
+// max runs of equal column degree the flooding MS kernel handles
+#define QLDPC_MAX_RUNS 8
 
 namespace qldpc {
 
@@ -35,8 +37,9 @@ struct DecodeArgs {
 };
 
 const void* select_kernel(int algo, bool layered, int dc);
-const void* select_ms_flood_kernel(int dc, int kc, int vp);  // nullptr if no instantiation fits
-int ms_flood_max_waves(int kc);
+// flooding MS, uniform row degree: global tables (fblob), LDS = wave state only
+const void* select_ms_flood_kernel(int dc, int kc);  // nullptr if no instantiation fits
+int ms_flood_max_waves(int kc);                      // waves per workgroup it was compiled for
 const void* select_ms_layered_kernel(int dc);                // layered MS, uniform degree (blob: layer tables)                               // waves per workgroup it was compiled for
 hipError_t launch_decode(const void* kernel, const DecodeArgs& args, int grid, int block,
                          int lds_bytes, hipStream_t stream);

@@ -52,6 +52,13 @@ __device__ __forceinline__ void wave_sync() {
 
 __device__ __forceinline__ uint64_t ballot(int pred) { return __ballot(pred); }
 
+// LDS (address space 3) access through a 32-bit byte address held in a VGPR
+// (ds_read / ds_write directly; a generic pointer would become flat_load).
+#define QLDPC_LDS(T, addr) ((__attribute__((address_space(3))) T*)(uintptr_t)(uint32_t)(addr))
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)p;
+}
+
 // NumPy DOUBLE_pairwise_sum over a contiguous LDS segment (np.sum of a 1-D
 // float64 array = 0.0 + pairwise(all); decoders.py:269, :276). n <= 128.
 __device__ __forceinline__ double np_pairwise_sum(const double* a, int n) {
@@ -114,6 +121,46 @@ __device__ __forceinline__ uint32_t opaque(uint32_t x) {
   return x;
 }
 
+__device__ __forceinline__ uint32_t opaque_always(uint32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+// v_min_f64 / v_max_f64 without the canonicalizes LLVM adds around
+// minnum/maxnum (operands here are never signalling NaNs).
+__device__ __forceinline__ double vmin_f64(double x, double y) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+  return r;
+}
+__device__ __forceinline__ double vmin_abs_f64(double x, double y) {  // min(|x|, y)
+  double r;
+  asm("v_min_f64 %0, |%1|, %2" : "=v"(r) : "v"(x), "v"(y));
+  return r;
+}
+__device__ __forceinline__ double vmax_abs_f64(double x, double y) {  // max(|x|, y)
+  double r;
+  asm("v_max_f64 %0, |%1|, %2" : "=v"(r) : "v"(x), "v"(y));
+  return r;
+}
+
+// XOR of N words as a balanced tree (v_xor3_b32-friendly)
+__device__ __forceinline__ uint32_t xor3(uint32_t x, uint32_t y, uint32_t z) {
+  uint32_t r;
+  // gfx950 has no v_xor3_b32; v_bitop3_b32 truth table 0x96 = S0 ^ S1 ^ S2
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(x), "v"(y), "v"(z));
+  return r;
+}
+template <int N>
+__device__ __forceinline__ uint32_t xor_tree(const uint32_t* w) {
+  if constexpr (N == 1) return w[0];
+  else if constexpr (N == 2) return w[0] ^ w[1];
+  else if constexpr (N == 3) return xor3(w[0], w[1], w[2]);
+  else if constexpr (N == 4) return xor3(w[0], w[1], w[2]) ^ w[3];
+  else if constexpr (N == 5) return xor3(xor3(w[0], w[1], w[2]), w[3], w[4]);
+  else return xor3(xor_tree<N - 2>(w), w[N - 2], w[N - 1]);
+}
+
 __device__ __forceinline__ uint32_t hi_word(double d) { return (uint32_t)(__builtin_bit_cast(uint64_t, d) >> 32); }
 
 // ---------------------------------------------------------------------------
@@ -159,50 +206,107 @@ __device__ __forceinline__ uint32_t cn_ms_uniform(const DecodeArgs& a, const uin
     }
     return 0;
   } else {
-    double v[NC][DC];
-    uint32_t ph[NC], sh[NC];
+    // Lean VALU form (the kernel is VALU-bound): the min / max go through
+    // inline v_min_f64 / v_max_f64 with an |x| source modifier (fmin/fmax
+    // would add a canonicalize per operand), the first argmin is tracked as
+    // its c2v address and v2c high word (no per-edge index compare at the
+    // output), c1/c2 are rounded once per check, and every edge is written
+    // with c1 before the argmin edge is overwritten with c2 (DS ops of a
+    // wave complete in order).
+    uint32_t hv[NC][DC], ph[NC], sh[NC], amin[NC], hmin[NC];
+    double min1[NC], min2[NC];
 #pragma unroll
     for (int q = 0; q < NC; ++q) {
-      ph[q] = 0;
-      sh[q] = 0;
+      double pj[DC], cv[DC];
 #pragma unroll
       for (int k = 0; k < DC; ++k) {
-        const double pj = *(const double*)(post_b + (t[q][k] & 0xffffu));
-        const float cv = *(const float*)(c2v_b + (t[q][k] >> 16));
-        v[q][k] = pj - (double)cv;                    // v2c = post - c2v (:177)
-        ph[q] ^= hi_word(pj);                         // hard decision post < 0 (:174)
-        sh[q] ^= hi_word(v[q][k]);                    // np.sign product (:157-159)
+        pj[k] = *(const double*)(post_b + (t[q][k] & 0xffffu));
+        cv[k] = (double)*(const float*)(c2v_b + (t[q][k] >> 16));
       }
+      min1[q] = __builtin_inf();
+      min2[q] = __builtin_inf();
+      uint32_t hp[DC];
+#pragma unroll
+      for (int k = 0; k < DC; ++k) {
+        const double v = pj[k] - cv[k];                   // v2c = post - c2v (:177)
+        hv[q][k] = hi_word(v);
+        hp[k] = hi_word(pj[k]);
+        if (k == 0) {
+          amin[q] = t[q][0] >> 16;                        // first argmin defaults to edge 0 (:161)
+          hmin[q] = hv[q][0];
+        }
+        const bool lt = __builtin_fabs(v) < min1[q];      // first argmin (:161)
+        amin[q] = lt ? (t[q][k] >> 16) : amin[q];
+        hmin[q] = lt ? hv[q][k] : hmin[q];
+        min2[q] = vmin_f64(min2[q], vmax_abs_f64(v, min1[q]));  // min of the rest (:162-164)
+        min1[q] = vmin_abs_f64(v, min1[q]);
+      }
+      ph[q] = xor_tree<DC>(hp);                           // hard-decision parity (:174)
+      sh[q] = xor_tree<DC>(hv[q]);                        // np.sign product (:157-159)
     }
     uint32_t unsat = 0;
 #pragma unroll
     for (int q = 0; q < NC; ++q) {
-      double min1 = __builtin_inf(), min2 = __builtin_inf();
-      int idx = 0;
-#pragma unroll
-      for (int k = 0; k < DC; ++k) {
-        const double av = __builtin_fabs(v[q][k]);
-        idx = (av < min1) ? k : idx;                  // first argmin (:161)
-        min2 = __builtin_fmin(min2, __builtin_fmax(min1, av));  // min of the rest (:162-164)
-        min1 = __builtin_fmin(min1, av);
-      }
-      if (__builtin_isinf(min1)) min1 = 0.0;          // (:165)
-      if (__builtin_isinf(min2)) min2 = 0.0;          // (:166)
-      if (min1 == 0.0 && live[q]) fl |= FLAG_MIN_ZERO;  // App. A.1.6 leak case (flagged)
-      const uint32_t negprod = ((sh[q] >> 31) ^ synb[q]) << 31;
-      const uint32_t c1 = __builtin_bit_cast(uint32_t, (float)(a.beta * min1));
-      const uint32_t c2 = __builtin_bit_cast(uint32_t, (float)(a.beta * min2));
+      double m1 = min1[q], m2 = min2[q];
+      if (__builtin_isinf(m1)) m1 = 0.0;                  // (:165)
+      if (__builtin_isinf(m2)) m2 = 0.0;                  // (:166)
+      if (m1 == 0.0 && live[q]) fl |= FLAG_MIN_ZERO;      // App. A.1.6 leak case (flagged)
+      const uint32_t npm = ((sh[q] >> 31) ^ synb[q]) << 31;
+      // c2v_e = fl32(beta * m_e), sign syn * prod * sign_e (:167-168)
+      const uint32_t c1n = opaque_always(__builtin_bit_cast(uint32_t, (float)(a.beta * m1)) ^ npm);
+      const uint32_t c2n = opaque_always(__builtin_bit_cast(uint32_t, (float)(a.beta * m2)) ^ npm);
       if (live[q]) {
 #pragma unroll
-        for (int k = 0; k < DC; ++k) {
-          const uint32_t mag = (k == idx) ? c2 : c1;  // (:167-168)
-          *(uint32_t*)(c2v_b + (t[q][k] >> 16)) = mag | ((hi_word(v[q][k]) ^ negprod) & 0x80000000u);
-        }
+        for (int k = 0; k < DC; ++k)
+          *(uint32_t*)(c2v_b + (t[q][k] >> 16)) = c1n ^ (hv[q][k] & 0x80000000u);
+        *(uint32_t*)(c2v_b + amin[q]) = c2n ^ (hmin[q] & 0x80000000u);
         unsat |= (ph[q] >> 31) ^ synb[q];
       }
     }
     return unsat;
   }
+}
+
+// Same check-node update as cn_ms_uniform<DC, false, 1> for one check whose
+// edges are given as absolute LDS byte addresses (pa: post f64, ca: c2v f32).
+// `live` = 0 for a pad check (its writes land in the pad; flags masked).
+template <int DC>
+__device__ __forceinline__ uint32_t cn_ms_abs(const DecodeArgs& a, const uint32_t* pa, const uint32_t* ca,
+                                              uint32_t synb, uint32_t live, int& fl) {
+  double pj[DC], cv[DC];
+#pragma unroll
+  for (int k = 0; k < DC; ++k) {
+    pj[k] = *QLDPC_LDS(const double, pa[k]);
+    cv[k] = (double)*QLDPC_LDS(const float, ca[k]);
+  }
+  double min1 = __builtin_inf(), min2 = __builtin_inf();
+  uint32_t hv[DC], hp[DC], amin = ca[0], hmin = 0;
+#pragma unroll
+  for (int k = 0; k < DC; ++k) {
+    const double v = pj[k] - cv[k];                       // v2c = post - c2v (:177)
+    hv[k] = hi_word(v);
+    hp[k] = hi_word(pj[k]);
+    if (k == 0) hmin = hv[0];                             // first argmin defaults to edge 0 (:161)
+    const bool lt = __builtin_fabs(v) < min1;             // first argmin (:161)
+    amin = lt ? ca[k] : amin;
+    hmin = lt ? hv[k] : hmin;
+    min2 = vmin_f64(min2, vmax_abs_f64(v, min1));         // min of the rest (:162-164)
+    min1 = vmin_abs_f64(v, min1);
+  }
+  const uint32_t ph = xor_tree<DC>(hp);                   // hard-decision parity (:174)
+  const uint32_t sh = xor_tree<DC>(hv);                   // np.sign product (:157-159)
+  if (__builtin_isinf(min1)) min1 = 0.0;                  // (:165)
+  if (__builtin_isinf(min2)) min2 = 0.0;                  // (:166)
+  if (min1 == 0.0 && live) fl |= FLAG_MIN_ZERO;           // App. A.1.6 leak case (flagged)
+  const uint32_t npm = ((sh >> 31) ^ synb) << 31;
+  // c2v_e = fl32(beta * m_e), sign syn * prod * sign_e (:167-168); every edge
+  // gets c1, then the argmin edge c2 (DS ops of a wave complete in order)
+  const uint32_t c1n = opaque_always(__builtin_bit_cast(uint32_t, (float)(a.beta * min1)) ^ npm);
+  const uint32_t c2n = opaque_always(__builtin_bit_cast(uint32_t, (float)(a.beta * min2)) ^ npm);
+#pragma unroll
+  for (int k = 0; k < DC; ++k) *QLDPC_LDS(uint32_t, ca[k]) = c1n ^ (hv[k] & 0x80000000u);
+  *QLDPC_LDS(uint32_t, amin) = c2n ^ (hmin & 0x80000000u);
+  return ((ph >> 31) ^ synb) & live;
 }
 
 // ---------------------------------------------------------------------------
@@ -325,6 +429,26 @@ __device__ __forceinline__ float ms_colsum(const float* c, int d) {
 #pragma unroll
   for (int t = 0; t < K; ++t) s += (t < d) ? x[t] : 0.0f;
   return s;
+}
+
+// VN column sum with a wave-uniform degree bound dmax (unrolled loads).
+__device__ __forceinline__ float ms_colsum_sw(const float* c, int d, int dmax) {
+  switch (dmax) {
+    case 0: return 0.0f;
+    case 1: return ms_colsum<1>(c, d);
+    case 2: return ms_colsum<2>(c, d);
+    case 3: return ms_colsum<3>(c, d);
+    case 4: return ms_colsum<4>(c, d);
+    case 5: return ms_colsum<5>(c, d);
+    case 6: return ms_colsum<6>(c, d);
+    case 7: return ms_colsum<7>(c, d);
+    case 8: return ms_colsum<8>(c, d);
+    default: {
+      float s = 0.0f;
+      for (int t = 0; t < d; ++t) s += c[t];
+      return s;
+    }
+  }
 }
 
 // dmax: wave-uniform upper bound of the degrees of the variables this pass
@@ -555,76 +679,97 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) decode_kernel(DecodeArgs a)
 }
 
 // ---------------------------------------------------------------------------
-// Flooding min-sum for uniform-degree codes with the lane's static graph data
-// held in VGPRs for the whole (persistent) kernel: the 8 table words of each
-// of its <= KC checks and the CSC start|degree word of each of its <= VP
-// variables. Each check-node step is then one LDS round trip (the gathers)
-// and each variable-node pass one round trip (the column). Same arithmetic
-// and results as decode_kernel<MS, false, DC>.
+// Flooding min-sum for uniform row degree DC <= 8 — the headline kernel.
+//
+// Differences from decode_kernel<MS, false, DC> (same arithmetic, same
+// results, bit for bit):
+//  * No graph tables in LDS. Each lane's static graph data comes once from
+//    HBM ("fblob", capi.cpp) and lives in VGPRs as ready-made LDS byte
+//    addresses: pa[i][k] = &post[var], ca[i][k] = &c2v[csc position] of edge
+//    k of check c = lane + 64 i. The check-node step then spends no VALU on
+//    addressing. Pad checks (c >= m) read post[0] and write the 8-float pad
+//    behind c2v; `livem` masks their flags.
+//  * Variable nodes are visited by runs of equal column degree K (variables
+//    are relabeled by degree, so the CSC start of variable start + o is
+//    p0 + o * K): no per-variable table, no masking, a compile-time K.
+// The LDS then holds only wave state: post f64[n] | c2v f32[E + 8].
 // ---------------------------------------------------------------------------
+struct FloodRuns {  // fblob header, read with scalar loads
+  int n_runs;
+  int start[QLDPC_MAX_RUNS], count[QLDPC_MAX_RUNS], deg[QLDPC_MAX_RUNS], p0[QLDPC_MAX_RUNS];
+};
+
 template <int K>
-__device__ __forceinline__ float ms_colsum_sw(const float* c, int d, int dmax) {
-  switch (dmax) {
-    case 0: return 0.0f;
-    case 1: return ms_colsum<1>(c, d);
-    case 2: return ms_colsum<2>(c, d);
-    case 3: return ms_colsum<3>(c, d);
-    case 4: return ms_colsum<4>(c, d);
-    case 5: return ms_colsum<5>(c, d);
-    case 6: return ms_colsum<6>(c, d);
-    case 7: return ms_colsum<7>(c, d);
-    case 8: return ms_colsum<8>(c, d);
-    default: {
+__device__ __forceinline__ void vn_run(const DecodeArgs& a, double* post, const float* c2v,
+                                       int start, int count, int p0, int lane) {
+  // post[start + o] = L + (f64) sum_t c2v[p0 + o K + t]   (decoders.py:172-173)
+  for (int o0 = 0; o0 < count; o0 += 64) {
+    const int o = o0 + lane;
+    if (o < count) {
       float s = 0.0f;
-      for (int t = 0; t < d; ++t) s += c[t];
-      return s;
+      if constexpr (K > 0) {
+        const float* c = c2v + p0 + o * K;
+        float x[K];
+#pragma unroll
+        for (int t = 0; t < K; ++t) x[t] = c[t];
+#pragma unroll
+        for (int t = 0; t < K; ++t) s += x[t];             // float32, ascending check
+      }
+      post[start + o] = a.L + (double)s;
     }
   }
 }
 
-// Large codes (KC = 8 checks per lane) keep 64 table words in VGPRs; their
-// per-wave LDS slice allows <= 2 waves per SIMD anyway, so they are compiled
-// for 512-thread workgroups (256 VGPRs) instead of 768.
-template <int KC>
-constexpr int ms_flood_max_threads() { return KC >= 8 ? 512 : QLDPC_MAX_THREADS; }
-
-template <int DC, int KC, int VP>
-__global__ void __launch_bounds__(ms_flood_max_threads<KC>()) ms_flood_kernel(DecodeArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  {
-    const uint4* src = (const uint4*)a.blob;
-    uint4* dst = (uint4*)lds;
-    const int nvec = a.blob_bytes >> 4;
-    for (int i = threadIdx.x; i < nvec; i += blockDim.x) dst[i] = src[i];
+__device__ __forceinline__ void vn_run_any(const DecodeArgs& a, double* post, const float* c2v,
+                                           int start, int count, int K, int p0, int lane) {
+  for (int o = lane; o < count; o += 64) {
+    const float* c = c2v + p0 + o * K;
+    float s = 0.0f;
+    for (int t = 0; t < K; ++t) s += c[t];
+    post[start + o] = a.L + (double)s;
   }
-  __syncthreads();
-  const uint32_t* cn_tab = (const uint32_t*)(lds + a.off_cn_tab);
-  const uint32_t* vn_info = (const uint32_t*)(lds + a.off_vn_ptr);
-  const uint8_t* chunk_dmax = (const uint8_t*)(lds + a.off_chunk_dmax);
+}
+
+template <int KC>
+constexpr int ms_flood_max_threads() { return KC >= 8 ? 512 : 256; }
+#ifndef QLDPC_FLOOD_WPE
+#define QLDPC_FLOOD_WPE 3  // waves per SIMD the register budget targets (KC <= 4)
+#endif
+template <int KC>
+constexpr int ms_flood_wpe() { return KC >= 8 ? 2 : QLDPC_FLOOD_WPE; }
+
+template <int DC, int KC>
+__global__ void __launch_bounds__(ms_flood_max_threads<KC>()) __attribute__((amdgpu_waves_per_eu(ms_flood_wpe<KC>())))
+ms_flood_kernel(DecodeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  static_assert(DC >= 2 && DC <= 8, "row degree 2..8");
+  const FloodRuns* runs = (const FloodRuns*)a.blob;                     // global, uniform
+  const uint32_t* ftab = (const uint32_t*)(a.blob + a.off_cn_tab);      // global
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int waves = blockDim.x >> 6;
-  unsigned char* ws = lds + a.blob_bytes + wid * a.wave_bytes;
+  unsigned char* ws = lds + wid * a.wave_bytes;
   double* post = (double*)ws;
   unsigned char* c2v_b = ws + a.off_c2v;
   const float* c2v_f = (const float*)c2v_b;
   const int m = a.m, n = a.n;
 
-  // static per-lane graph data (registers for the whole kernel)
-  uint32_t tr[KC][8];
+  // static per-lane graph data: absolute LDS addresses (VGPRs for the kernel)
+  uint32_t pa[KC][8], ca[KC][8];
+  uint32_t livem = 0;
+  const uint32_t wbase = lds_addr(ws);
 #pragma unroll
   for (int i = 0; i < KC; ++i) {
-    const int c = lane + 64 * i;
-    load_row8(cn_tab + (c < m ? c : m - 1) * 8, tr[i]);
-  }
-  uint32_t vi[VP];
-  int dm[VP];
+    uint32_t t[8];
+    load_row8(ftab + (size_t)(lane + 64 * i) * 8, t);
 #pragma unroll
-  for (int q = 0; q < VP; ++q) {
-    const int j = lane + 64 * q;
-    vi[q] = j < n ? vn_info[j] : 0u;
-    dm[q] = 64 * q < n ? __builtin_amdgcn_readfirstlane((int)chunk_dmax[q]) : 0;
+    for (int k = 0; k < 8; ++k) {
+      pa[i][k] = wbase + (t[k] & 0xffffu);
+      ca[i][k] = wbase + (uint32_t)a.off_c2v + (t[k] >> 16);
+    }
+    if (lane + 64 * i < m) livem |= 1u << i;
   }
+  const int n_runs = runs->n_runs;
 
   for (long long hs = (long long)blockIdx.x * waves + wid; hs < a.batch;
        hs += (long long)gridDim.x * waves) {
@@ -641,24 +786,25 @@ __global__ void __launch_bounds__(ms_flood_max_threads<KC>()) ms_flood_kernel(De
     for (int it = 0;; ++it) {
       uint32_t unsat = 0;
       if (it == 0) {
+        // every v2c = float32(L) (decoders.py:148-149): one value per check
+        const double vf = (double)a.L32;
+        const double av = __builtin_fabs(vf);
+        const uint32_t cb = __builtin_bit_cast(uint32_t, (float)(a.beta * av));
+        const uint32_t neg = (uint32_t)(vf < 0.0);
+        if (av == 0.0) fl |= FLAG_MIN_ZERO;
 #pragma unroll
         for (int i = 0; i < KC; ++i) {
-          const bool live[1] = {lane + 64 * i < m};
-          const uint32_t sb[1] = {(synreg >> i) & 1u};
-          uint32_t t[1][8];
+          const uint32_t negprod = ((neg * DC) ^ (synreg >> i)) & 1u;
+          const uint32_t val = cb | ((neg ^ negprod) << 31);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) t[0][k] = opaque<1>(tr[i][k]);
-          (void)cn_ms_uniform<DC, true, 1>(a, t, sb, live, (const unsigned char*)post, c2v_b, fl);
+          for (int k = 0; k < DC; ++k) *QLDPC_LDS(uint32_t, ca[i][k]) = val;
         }
       } else {
 #pragma unroll
         for (int i = 0; i < KC; ++i) {
-          const bool live[1] = {lane + 64 * i < m};
+          const uint32_t live[1] = {(livem >> i) & 1u};
           const uint32_t sb[1] = {(synreg >> i) & 1u};
-          uint32_t t[1][8];
-#pragma unroll
-          for (int k = 0; k < 8; ++k) t[0][k] = opaque<1>(tr[i][k]);
-          unsat |= cn_ms_uniform<DC, false, 1>(a, t, sb, live, (const unsigned char*)post, c2v_b, fl);
+          unsat |= cn_ms_abs<DC>(a, pa[i], ca[i], sb[0], live[0], fl);
           __builtin_amdgcn_sched_barrier(0);         // one check's working set at a time
         }
         // stop test of iteration it-1 (decoders.py:175-176)
@@ -669,15 +815,18 @@ __global__ void __launch_bounds__(ms_flood_max_threads<KC>()) ms_flood_kernel(De
         }
       }
       wave_sync();
-#pragma unroll
-      for (int q = 0; q < VP; ++q) {
-        if (64 * q < n) {                            // wave-uniform
-          const int j = lane + 64 * q;
-          const uint32_t w = opaque<2>(vi[q]);
-          const float s = ms_colsum_sw<0>(c2v_f + (w & 0xffffu), (int)(w >> 16), dm[q]);
-          if (j < n) post[j] = a.L + (double)s;      // (:172-173)
+      for (int r = 0; r < n_runs; ++r) {
+        const int st = runs->start[r], cnt = runs->count[r], K = runs->deg[r], p0 = runs->p0[r];
+        switch (K) {
+          case 0: vn_run<0>(a, post, c2v_f, st, cnt, p0, lane); break;
+          case 1: vn_run<1>(a, post, c2v_f, st, cnt, p0, lane); break;
+          case 2: vn_run<2>(a, post, c2v_f, st, cnt, p0, lane); break;
+          case 3: vn_run<3>(a, post, c2v_f, st, cnt, p0, lane); break;
+          case 4: vn_run<4>(a, post, c2v_f, st, cnt, p0, lane); break;
+          case 5: vn_run<5>(a, post, c2v_f, st, cnt, p0, lane); break;
+          case 6: vn_run<6>(a, post, c2v_f, st, cnt, p0, lane); break;
+          default: vn_run_any(a, post, c2v_f, st, cnt, K, p0, lane); break;
         }
-        __builtin_amdgcn_sched_barrier(0);
       }
       wave_sync();
       if (it + 1 == a.max_iter) {
@@ -686,8 +835,8 @@ __global__ void __launch_bounds__(ms_flood_max_threads<KC>()) ms_flood_kernel(De
         for (int i = 0; i < KC; ++i) {
           uint32_t ph = 0;
 #pragma unroll
-          for (int k = 0; k < DC; ++k) ph ^= hi_word(*(const double*)((const unsigned char*)post + (opaque<1>(tr[i][k]) & 0xffffu)));
-          if (lane + 64 * i < m) un |= (ph >> 31) ^ ((synreg >> i) & 1u);
+          for (int k = 0; k < DC; ++k) ph ^= hi_word(*QLDPC_LDS(const double, pa[i][k]));
+          un |= (((ph >> 31) ^ (synreg >> i)) & (livem >> i)) & 1u;
         }
         conv = ballot(un != 0) == 0;
         break;
@@ -708,6 +857,7 @@ __global__ void __launch_bounds__(ms_flood_max_threads<KC>()) ms_flood_kernel(De
     wave_sync();
   }
 }
+
 
 // ---------------------------------------------------------------------------
 // Layered / serial min-sum for uniform-degree codes (decoders.py:153-177 with
@@ -788,7 +938,7 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
           const uint32_t info = adj_info[q];
           const int j = (int)(info >> 21), d = (int)((info >> 16) & 31u);
           const double old = post[j];
-          const float s = ms_colsum_sw<0>(c2v + (info & 0xffffu), d, dmax);
+          const float s = ms_colsum_sw(c2v + (info & 0xffffu), d, dmax);
           const double nw = L + (double)s;
           post[j] = nw;
           if ((old < 0.0) != (nw < 0.0)) {                       // hard decision flipped
@@ -832,16 +982,16 @@ static const void* kernel_ptr() {
   return (const void*)&decode_kernel<ALGO, LAYERED, DC>;
 }
 
-int ms_flood_max_waves(int kc) { return (kc > 4 ? 512 : QLDPC_MAX_THREADS) / 64; }
+int ms_flood_max_waves(int kc) { return (kc >= 8 ? 512 : 256) / 64; }
 
-const void* select_ms_flood_kernel(int dc, int kc, int vp) {
-  // instantiated (DC, KC, VP) shapes; the host passes the smallest that covers
-  // ceil(m/64) checks and ceil(n/64) variable passes per lane
-  if (dc == 7 && kc <= 2 && vp <= 4) return (const void*)&ms_flood_kernel<7, 2, 4>;
-  if (dc == 7 && kc <= 4 && vp <= 9) return (const void*)&ms_flood_kernel<7, 4, 9>;
-  if (dc == 8 && kc <= 4 && vp <= 9) return (const void*)&ms_flood_kernel<8, 4, 9>;
-  if (dc == 7 && kc <= 8 && vp <= 17) return (const void*)&ms_flood_kernel<7, 8, 17>;
-  if (dc == 8 && kc <= 8 && vp <= 17) return (const void*)&ms_flood_kernel<8, 8, 17>;
+const void* select_ms_flood_kernel(int dc, int kc) {
+  // instantiated (DC, KC) shapes; the host passes ceil(m/64) checks per lane
+  if (dc == 7 && kc <= 2) return (const void*)&ms_flood_kernel<7, 2>;
+  if (dc == 8 && kc <= 2) return (const void*)&ms_flood_kernel<8, 2>;
+  if (dc == 7 && kc <= 4) return (const void*)&ms_flood_kernel<7, 4>;
+  if (dc == 8 && kc <= 4) return (const void*)&ms_flood_kernel<8, 4>;
+  if (dc == 7 && kc <= 8) return (const void*)&ms_flood_kernel<7, 8>;
+  if (dc == 8 && kc <= 8) return (const void*)&ms_flood_kernel<8, 8>;
   return nullptr;
 }
 
