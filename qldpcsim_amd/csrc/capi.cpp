@@ -466,7 +466,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   HIP_TRY(hipGetDevice(&dev));
   HIP_TRY(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
   HIP_TRY(qldpc::configure_kernel(cfg.kernel, max_lds));
-  const int blob = gtab ? 0 : (int)(use_lblob ? s->lblob.size() : s->blob.size());
+  const int blob = gtab ? QLDPC_FLOOD_HDR : (int)(use_lblob ? s->lblob.size() : s->blob.size());
   int best_waves = 0;
   for (int w = max_waves; w >= 1; --w) {
     const int lds = blob + w * cfg.wave_bytes;

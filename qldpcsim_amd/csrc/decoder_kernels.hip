@@ -273,43 +273,41 @@ __device__ __forceinline__ uint32_t cn_ms_uniform(const DecodeArgs& a, const uin
 template <int DC>
 __device__ __forceinline__ uint32_t cn_ms_abs(const DecodeArgs& a, const uint32_t* pa, const uint32_t* ca,
                                               uint32_t synb, uint32_t live, int& fl) {
-  double pj[DC], cv[DC];
+  double pj[DC], v[DC];
 #pragma unroll
   for (int k = 0; k < DC; ++k) {
     pj[k] = *QLDPC_LDS(const double, pa[k]);
-    cv[k] = (double)*QLDPC_LDS(const float, ca[k]);
+    v[k] = (double)*QLDPC_LDS(const float, ca[k]);
   }
   double min1 = __builtin_inf(), min2 = __builtin_inf();
-  uint32_t hv[DC], hp[DC], amin = ca[0], hmin = 0;
+  uint32_t hv[DC], hp[DC];
 #pragma unroll
   for (int k = 0; k < DC; ++k) {
-    const double v = pj[k] - cv[k];                       // v2c = post - c2v (:177)
-    hv[k] = hi_word(v);
+    v[k] = pj[k] - v[k];                                  // v2c = post - c2v (:177)
+    hv[k] = hi_word(v[k]);
     hp[k] = hi_word(pj[k]);
-    if (k == 0) hmin = hv[0];                             // first argmin defaults to edge 0 (:161)
-    const bool lt = __builtin_fabs(v) < min1;             // first argmin (:161)
-    amin = lt ? ca[k] : amin;
-    hmin = lt ? hv[k] : hmin;
-    min2 = vmin_f64(min2, vmax_abs_f64(v, min1));         // min of the rest (:162-164)
-    min1 = vmin_abs_f64(v, min1);
+    min2 = vmin_f64(min2, vmax_abs_f64(v[k], min1));      // min of the rest (:162-164)
+    min1 = vmin_abs_f64(v[k], min1);
   }
   const uint32_t ph = xor_tree<DC>(hp);                   // hard-decision parity (:174)
   const uint32_t sh = xor_tree<DC>(hv);                   // np.sign product (:157-159)
-  if (__builtin_isinf(min1)) min1 = 0.0;                  // (:165)
-  if (__builtin_isinf(min2)) min2 = 0.0;                  // (:166)
-  if (min1 == 0.0 && live) fl |= FLAG_MIN_ZERO;           // App. A.1.6 leak case (flagged)
+  const double m1 = __builtin_isinf(min1) ? 0.0 : min1;   // (:165)
+  const double m2 = __builtin_isinf(min2) ? 0.0 : min2;   // (:166)
+  if (m1 == 0.0 && live) fl |= FLAG_MIN_ZERO;             // App. A.1.6 leak case (flagged)
   const uint32_t npm = ((sh >> 31) ^ synb) << 31;
-  // c2v_e = fl32(beta * m_e), sign syn * prod * sign_e (:167-168); every edge
-  // gets c1, then the argmin edge c2 (DS ops of a wave complete in order)
-  const uint32_t c1n = opaque_always(__builtin_bit_cast(uint32_t, (float)(a.beta * min1)) ^ npm);
-  const uint32_t c2n = opaque_always(__builtin_bit_cast(uint32_t, (float)(a.beta * min2)) ^ npm);
+  // c2v_e = fl32(beta * (|v_e| == min1 ? min2 : min1)), sign syn * prod *
+  // sign_e (:167-168). The reference gives min2 to the first argmin only;
+  // "every edge equal to min1" is the same thing: with a tie min2 == min1.
+  const uint32_t c1n = opaque_always(__builtin_bit_cast(uint32_t, (float)(a.beta * m1)) ^ npm);
+  const uint32_t c2n = opaque_always(__builtin_bit_cast(uint32_t, (float)(a.beta * m2)) ^ npm);
 #pragma unroll
-  for (int k = 0; k < DC; ++k) *QLDPC_LDS(uint32_t, ca[k]) = c1n ^ (hv[k] & 0x80000000u);
-  *QLDPC_LDS(uint32_t, amin) = c2n ^ (hmin & 0x80000000u);
+  for (int k = 0; k < DC; ++k) {
+    const uint32_t c = (__builtin_fabs(v[k]) == min1) ? c2n : c1n;
+    *QLDPC_LDS(uint32_t, ca[k]) = c ^ (hv[k] & 0x80000000u);
+  }
   return ((ph >> 31) ^ synb) & live;
 }
 
-// ---------------------------------------------------------------------------
 // Check-node update of one check `c` (lane-local), any degree.
 //   MS: decoders.py:155-169.  BP: decoders.py:249-262.
 // Returns the check's current parity XOR syndrome bit ("unsatisfied"),
@@ -694,7 +692,7 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) decode_kernel(DecodeArgs a)
 //    p0 + o * K): no per-variable table, no masking, a compile-time K.
 // The LDS then holds only wave state: post f64[n] | c2v f32[E + 8].
 // ---------------------------------------------------------------------------
-struct FloodRuns {  // fblob header, read with scalar loads
+struct FloodRuns {  // fblob header: runs of equal column degree (capi.cpp)
   int n_runs;
   int start[QLDPC_MAX_RUNS], count[QLDPC_MAX_RUNS], deg[QLDPC_MAX_RUNS], p0[QLDPC_MAX_RUNS];
 };
@@ -748,7 +746,7 @@ ms_flood_kernel(DecodeArgs a) {
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int waves = blockDim.x >> 6;
-  unsigned char* ws = lds + wid * a.wave_bytes;
+  unsigned char* ws = lds + QLDPC_FLOOD_HDR + wid * a.wave_bytes;
   double* post = (double*)ws;
   unsigned char* c2v_b = ws + a.off_c2v;
   const float* c2v_f = (const float*)c2v_b;
@@ -769,7 +767,12 @@ ms_flood_kernel(DecodeArgs a) {
     }
     if (lane + 64 * i < m) livem |= 1u << i;
   }
-  const int n_runs = runs->n_runs;
+  // the runs header lives in LDS (the first QLDPC_FLOOD_HDR bytes): one
+  // broadcast read per field per iteration, no global latency in the loop
+  const int n_runs = __builtin_amdgcn_readfirstlane(runs->n_runs);
+  if (threadIdx.x < 4 * QLDPC_MAX_RUNS) ((int*)lds)[threadIdx.x] = (&runs->start[0])[threadIdx.x];
+  __syncthreads();
+  const int* hdr = (const int*)lds;
 
   for (long long hs = (long long)blockIdx.x * waves + wid; hs < a.batch;
        hs += (long long)gridDim.x * waves) {
@@ -816,7 +819,10 @@ ms_flood_kernel(DecodeArgs a) {
       }
       wave_sync();
       for (int r = 0; r < n_runs; ++r) {
-        const int st = runs->start[r], cnt = runs->count[r], K = runs->deg[r], p0 = runs->p0[r];
+        const int st = __builtin_amdgcn_readfirstlane(hdr[r]);
+        const int cnt = __builtin_amdgcn_readfirstlane(hdr[QLDPC_MAX_RUNS + r]);
+        const int K = __builtin_amdgcn_readfirstlane(hdr[2 * QLDPC_MAX_RUNS + r]);
+        const int p0 = __builtin_amdgcn_readfirstlane(hdr[3 * QLDPC_MAX_RUNS + r]);
         switch (K) {
           case 0: vn_run<0>(a, post, c2v_f, st, cnt, p0, lane); break;
           case 1: vn_run<1>(a, post, c2v_f, st, cnt, p0, lane); break;
