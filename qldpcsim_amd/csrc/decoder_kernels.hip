@@ -144,6 +144,44 @@ __device__ __forceinline__ double vmax_abs_f64(double x, double y) {  // max(|x|
   return r;
 }
 
+__device__ __forceinline__ double vmin_abs2_f64(double x, double y) {  // min(|x|, |y|)
+  double r;
+  asm("v_min_f64 %0, |%1|, |%2|" : "=v"(r) : "v"(x), "v"(y));
+  return r;
+}
+__device__ __forceinline__ double vmax_abs2_f64(double x, double y) {  // max(|x|, |y|)
+  double r;
+  asm("v_max_f64 %0, |%1|, |%2|" : "=v"(r) : "v"(x), "v"(y));
+  return r;
+}
+__device__ __forceinline__ double vmax_f64(double x, double y) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+  return r;
+}
+
+// Smallest and second smallest (with multiplicity) of |v[0..N)| as a
+// tournament: pairs, then merges (l1,h1)+(l2,h2) -> (min(l1,l2),
+// min(max(l1,l2), min(h1,h2))). Depth ~log2 N instead of a serial chain
+// (the check-node step is latency-bound), and fewer ops than the chain.
+template <int N>
+__device__ __forceinline__ void min12_tree(const double* v, double& lo, double& hi) {
+  if constexpr (N == 1) {
+    lo = __builtin_fabs(v[0]);
+    hi = __builtin_inf();
+  } else if constexpr (N == 2) {
+    lo = vmin_abs2_f64(v[0], v[1]);
+    hi = vmax_abs2_f64(v[0], v[1]);
+  } else {
+    constexpr int H = (N / 2 + 1) & ~1;   // even split: 3->2+1, 5->2+3, 6->4+2, 7->4+3, 8->4+4
+    double l1, h1, l2, h2;
+    min12_tree<(H < N ? H : N - 1)>(v, l1, h1);
+    min12_tree<N - (H < N ? H : N - 1)>(v + (H < N ? H : N - 1), l2, h2);
+    lo = vmin_f64(l1, l2);
+    hi = vmin_f64(vmax_f64(l1, l2), vmin_f64(h1, h2));
+  }
+}
+
 // XOR of N words as a balanced tree (v_xor3_b32-friendly)
 __device__ __forceinline__ uint32_t xor3(uint32_t x, uint32_t y, uint32_t z) {
   uint32_t r;
@@ -279,16 +317,15 @@ __device__ __forceinline__ uint32_t cn_ms_abs(const DecodeArgs& a, const uint32_
     pj[k] = *QLDPC_LDS(const double, pa[k]);
     v[k] = (double)*QLDPC_LDS(const float, ca[k]);
   }
-  double min1 = __builtin_inf(), min2 = __builtin_inf();
   uint32_t hv[DC], hp[DC];
 #pragma unroll
   for (int k = 0; k < DC; ++k) {
     v[k] = pj[k] - v[k];                                  // v2c = post - c2v (:177)
     hv[k] = hi_word(v[k]);
     hp[k] = hi_word(pj[k]);
-    min2 = vmin_f64(min2, vmax_abs_f64(v[k], min1));      // min of the rest (:162-164)
-    min1 = vmin_abs_f64(v[k], min1);
   }
+  double min1, min2;                                      // first min / min of the rest (:160-164)
+  min12_tree<DC>(v, min1, min2);
   const uint32_t ph = xor_tree<DC>(hp);                   // hard-decision parity (:174)
   const uint32_t sh = xor_tree<DC>(hv);                   // np.sign product (:157-159)
   const double m1 = __builtin_isinf(min1) ? 0.0 : min1;   // (:165)
@@ -808,7 +845,9 @@ ms_flood_kernel(DecodeArgs a) {
           const uint32_t live[1] = {(livem >> i) & 1u};
           const uint32_t sb[1] = {(synreg >> i) & 1u};
           unsat |= cn_ms_abs<DC>(a, pa[i], ca[i], sb[0], live[0], fl);
+#ifndef QLDPC_FLOOD_NOBAR
           __builtin_amdgcn_sched_barrier(0);         // one check's working set at a time
+#endif
         }
         // stop test of iteration it-1 (decoders.py:175-176)
         if (ballot(unsat != 0) == 0) {
