@@ -735,24 +735,37 @@ struct FloodRuns {  // fblob header: runs of equal column degree (capi.cpp)
 };
 
 template <int K>
+__device__ __forceinline__ float vn_sum(const float* c) {
+  float s = 0.0f;
+  if constexpr (K > 0) {
+    float x[K];
+#pragma unroll
+    for (int t = 0; t < K; ++t) x[t] = c[t];
+#pragma unroll
+    for (int t = 0; t < K; ++t) s += x[t];               // float32, ascending check
+  }
+  return s;
+}
+
+template <int K>
 __device__ __forceinline__ void vn_run(const DecodeArgs& a, double* post, const float* c2v,
                                        int start, int count, int p0, int lane) {
   // post[start + o] = L + (f64) sum_t c2v[p0 + o K + t]   (decoders.py:172-173)
-  for (int o0 = 0; o0 < count; o0 += 64) {
-    const int o = o0 + lane;
-    if (o < count) {
-      float s = 0.0f;
-      if constexpr (K > 0) {
-        const float* c = c2v + p0 + o * K;
-        float x[K];
-#pragma unroll
-        for (int t = 0; t < K; ++t) x[t] = c[t];
-#pragma unroll
-        for (int t = 0; t < K; ++t) s += x[t];             // float32, ascending check
-      }
-      post[start + o] = a.L + (double)s;
-    }
+  // Full 64-variable chunks two at a time (two independent add chains in
+  // flight), then the masked tail.
+  const float* c = c2v + p0 + lane * K;
+  double* po = post + start + lane;
+  int o0 = 0;
+#ifndef QLDPC_VN_NOPAIR
+  for (; o0 + 128 <= count; o0 += 128) {
+    const float s0 = vn_sum<K>(c + o0 * K);
+    const float s1 = vn_sum<K>(c + (o0 + 64) * K);
+    po[o0] = a.L + (double)s0;
+    po[o0 + 64] = a.L + (double)s1;
   }
+#endif
+  for (; o0 + 64 <= count; o0 += 64) po[o0] = a.L + (double)vn_sum<K>(c + o0 * K);
+  if (o0 + lane < count) po[o0] = a.L + (double)vn_sum<K>(c + o0 * K);
 }
 
 __device__ __forceinline__ void vn_run_any(const DecodeArgs& a, double* post, const float* c2v,
