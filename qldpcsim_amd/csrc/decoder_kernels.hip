@@ -218,6 +218,64 @@ __device__ __forceinline__ void load_row8(const uint32_t* tab, uint32_t (&t)[8])
   t[4] = t1.x; t[5] = t1.y; t[6] = t1.z; t[7] = t1.w;
 }
 
+// Min-sum check-node update of one uniform-degree check (decoders.py:155-169)
+// whose edges are given as absolute LDS byte addresses (pa: post f64, ca: c2v
+// f32). `live` = 0 for a pad check (its writes land in the pad; flags masked).
+template <int DC>
+struct CnLoad {
+  double pj[DC];
+  float cv[DC];
+};
+
+template <int DC>
+__device__ __forceinline__ void cn_ms_load(CnLoad<DC>& L, const uint32_t* pa, const uint32_t* ca) {
+#pragma unroll
+  for (int k = 0; k < DC; ++k) {
+    L.pj[k] = *QLDPC_LDS(const double, pa[k]);
+    L.cv[k] = *QLDPC_LDS(const float, ca[k]);
+  }
+}
+
+template <int DC>
+__device__ __forceinline__ uint32_t cn_ms_compute(const DecodeArgs& a, const CnLoad<DC>& L, const uint32_t* ca,
+                                                  uint32_t synb, uint32_t live, int& fl) {
+  double v[DC];
+  uint32_t hv[DC], hp[DC];
+#pragma unroll
+  for (int k = 0; k < DC; ++k) {
+    v[k] = L.pj[k] - (double)L.cv[k];                     // v2c = post - c2v (:177)
+    hv[k] = hi_word(v[k]);
+    hp[k] = hi_word(L.pj[k]);
+  }
+  double min1, min2;                                      // first min / min of the rest (:160-164)
+  min12_tree<DC>(v, min1, min2);
+  const uint32_t ph = xor_tree<DC>(hp);                   // hard-decision parity (:174)
+  const uint32_t sh = xor_tree<DC>(hv);                   // np.sign product (:157-159)
+  const double m1 = __builtin_isinf(min1) ? 0.0 : min1;   // (:165)
+  const double m2 = __builtin_isinf(min2) ? 0.0 : min2;   // (:166)
+  if (m1 == 0.0 && live) fl |= FLAG_MIN_ZERO;             // App. A.1.6 leak case (flagged)
+  const uint32_t npm = ((sh >> 31) ^ synb) << 31;
+  // c2v_e = fl32(beta * (|v_e| == min1 ? min2 : min1)), sign syn * prod *
+  // sign_e (:167-168). The reference gives min2 to the first argmin only;
+  // "every edge equal to min1" is the same thing: with a tie min2 == min1.
+  const uint32_t c1n = opaque_always(__builtin_bit_cast(uint32_t, (float)(a.beta * m1)) ^ npm);
+  const uint32_t c2n = opaque_always(__builtin_bit_cast(uint32_t, (float)(a.beta * m2)) ^ npm);
+#pragma unroll
+  for (int k = 0; k < DC; ++k) {
+    const uint32_t c = (__builtin_fabs(v[k]) == min1) ? c2n : c1n;
+    *QLDPC_LDS(uint32_t, ca[k]) = c ^ (hv[k] & 0x80000000u);
+  }
+  return ((ph >> 31) ^ synb) & live;
+}
+
+template <int DC>
+__device__ __forceinline__ uint32_t cn_ms_abs(const DecodeArgs& a, const uint32_t* pa, const uint32_t* ca,
+                                              uint32_t synb, uint32_t live, int& fl) {
+  CnLoad<DC> L;
+  cn_ms_load<DC>(L, pa, ca);
+  return cn_ms_compute<DC>(a, L, ca, synb, live, fl);
+}
+
 // NC independent checks per call: every LDS read of all NC checks is issued
 // before any arithmetic. `t[q]` holds check q's 8 table words (registers).
 template <int DC, bool FIRST, int NC>
@@ -244,105 +302,26 @@ __device__ __forceinline__ uint32_t cn_ms_uniform(const DecodeArgs& a, const uin
     }
     return 0;
   } else {
-    // Lean VALU form (the kernel is VALU-bound): the min / max go through
-    // inline v_min_f64 / v_max_f64 with an |x| source modifier (fmin/fmax
-    // would add a canonicalize per operand), the first argmin is tracked as
-    // its c2v address and v2c high word (no per-edge index compare at the
-    // output), c1/c2 are rounded once per check, and every edge is written
-    // with c1 before the argmin edge is overwritten with c2 (DS ops of a
-    // wave complete in order).
-    uint32_t hv[NC][DC], ph[NC], sh[NC], amin[NC], hmin[NC];
-    double min1[NC], min2[NC];
-#pragma unroll
-    for (int q = 0; q < NC; ++q) {
-      double pj[DC], cv[DC];
-#pragma unroll
-      for (int k = 0; k < DC; ++k) {
-        pj[k] = *(const double*)(post_b + (t[q][k] & 0xffffu));
-        cv[k] = (double)*(const float*)(c2v_b + (t[q][k] >> 16));
-      }
-      min1[q] = __builtin_inf();
-      min2[q] = __builtin_inf();
-      uint32_t hp[DC];
-#pragma unroll
-      for (int k = 0; k < DC; ++k) {
-        const double v = pj[k] - cv[k];                   // v2c = post - c2v (:177)
-        hv[q][k] = hi_word(v);
-        hp[k] = hi_word(pj[k]);
-        if (k == 0) {
-          amin[q] = t[q][0] >> 16;                        // first argmin defaults to edge 0 (:161)
-          hmin[q] = hv[q][0];
-        }
-        const bool lt = __builtin_fabs(v) < min1[q];      // first argmin (:161)
-        amin[q] = lt ? (t[q][k] >> 16) : amin[q];
-        hmin[q] = lt ? hv[q][k] : hmin[q];
-        min2[q] = vmin_f64(min2[q], vmax_abs_f64(v, min1[q]));  // min of the rest (:162-164)
-        min1[q] = vmin_abs_f64(v, min1[q]);
-      }
-      ph[q] = xor_tree<DC>(hp);                           // hard-decision parity (:174)
-      sh[q] = xor_tree<DC>(hv[q]);                        // np.sign product (:157-159)
-    }
+    // the flooding kernel's check node (cn_ms_load / cn_ms_compute) on
+    // addresses formed from the packed table words
     uint32_t unsat = 0;
+    const uint32_t pb = lds_addr(post_b), cb = lds_addr(c2v_b);
 #pragma unroll
     for (int q = 0; q < NC; ++q) {
-      double m1 = min1[q], m2 = min2[q];
-      if (__builtin_isinf(m1)) m1 = 0.0;                  // (:165)
-      if (__builtin_isinf(m2)) m2 = 0.0;                  // (:166)
-      if (m1 == 0.0 && live[q]) fl |= FLAG_MIN_ZERO;      // App. A.1.6 leak case (flagged)
-      const uint32_t npm = ((sh[q] >> 31) ^ synb[q]) << 31;
-      // c2v_e = fl32(beta * m_e), sign syn * prod * sign_e (:167-168)
-      const uint32_t c1n = opaque_always(__builtin_bit_cast(uint32_t, (float)(a.beta * m1)) ^ npm);
-      const uint32_t c2n = opaque_always(__builtin_bit_cast(uint32_t, (float)(a.beta * m2)) ^ npm);
-      if (live[q]) {
+      uint32_t pa[8], ca[8];
 #pragma unroll
-        for (int k = 0; k < DC; ++k)
-          *(uint32_t*)(c2v_b + (t[q][k] >> 16)) = c1n ^ (hv[q][k] & 0x80000000u);
-        *(uint32_t*)(c2v_b + amin[q]) = c2n ^ (hmin[q] & 0x80000000u);
-        unsat |= (ph[q] >> 31) ^ synb[q];
+      for (int k = 0; k < 8; ++k) {
+        pa[k] = pb + (t[q][k] & 0xffffu);
+        ca[k] = cb + (t[q][k] >> 16);
+      }
+      if (live[q]) {
+        CnLoad<DC> L;
+        cn_ms_load<DC>(L, pa, ca);
+        unsat |= cn_ms_compute<DC>(a, L, ca, synb[q], 1u, fl);
       }
     }
     return unsat;
   }
-}
-
-// Same check-node update as cn_ms_uniform<DC, false, 1> for one check whose
-// edges are given as absolute LDS byte addresses (pa: post f64, ca: c2v f32).
-// `live` = 0 for a pad check (its writes land in the pad; flags masked).
-template <int DC>
-__device__ __forceinline__ uint32_t cn_ms_abs(const DecodeArgs& a, const uint32_t* pa, const uint32_t* ca,
-                                              uint32_t synb, uint32_t live, int& fl) {
-  double pj[DC], v[DC];
-#pragma unroll
-  for (int k = 0; k < DC; ++k) {
-    pj[k] = *QLDPC_LDS(const double, pa[k]);
-    v[k] = (double)*QLDPC_LDS(const float, ca[k]);
-  }
-  uint32_t hv[DC], hp[DC];
-#pragma unroll
-  for (int k = 0; k < DC; ++k) {
-    v[k] = pj[k] - v[k];                                  // v2c = post - c2v (:177)
-    hv[k] = hi_word(v[k]);
-    hp[k] = hi_word(pj[k]);
-  }
-  double min1, min2;                                      // first min / min of the rest (:160-164)
-  min12_tree<DC>(v, min1, min2);
-  const uint32_t ph = xor_tree<DC>(hp);                   // hard-decision parity (:174)
-  const uint32_t sh = xor_tree<DC>(hv);                   // np.sign product (:157-159)
-  const double m1 = __builtin_isinf(min1) ? 0.0 : min1;   // (:165)
-  const double m2 = __builtin_isinf(min2) ? 0.0 : min2;   // (:166)
-  if (m1 == 0.0 && live) fl |= FLAG_MIN_ZERO;             // App. A.1.6 leak case (flagged)
-  const uint32_t npm = ((sh >> 31) ^ synb) << 31;
-  // c2v_e = fl32(beta * (|v_e| == min1 ? min2 : min1)), sign syn * prod *
-  // sign_e (:167-168). The reference gives min2 to the first argmin only;
-  // "every edge equal to min1" is the same thing: with a tie min2 == min1.
-  const uint32_t c1n = opaque_always(__builtin_bit_cast(uint32_t, (float)(a.beta * m1)) ^ npm);
-  const uint32_t c2n = opaque_always(__builtin_bit_cast(uint32_t, (float)(a.beta * m2)) ^ npm);
-#pragma unroll
-  for (int k = 0; k < DC; ++k) {
-    const uint32_t c = (__builtin_fabs(v[k]) == min1) ? c2n : c1n;
-    *QLDPC_LDS(uint32_t, ca[k]) = c ^ (hv[k] & 0x80000000u);
-  }
-  return ((ph >> 31) ^ synb) & live;
 }
 
 // Check-node update of one check `c` (lane-local), any degree.
@@ -729,6 +708,57 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) decode_kernel(DecodeArgs a)
 //    p0 + o * K): no per-variable table, no masking, a compile-time K.
 // The LDS then holds only wave state: post f64[n] | c2v f32[E + 8].
 // ---------------------------------------------------------------------------
+#ifndef QLDPC_FLOOD_PACKED
+#define QLDPC_FLOOD_PACKED false
+#endif
+// Per-lane edge addresses of the KC checks a lane owns. Absolute: 16 VGPRs
+// per check, no VALU per use. Packed: the table words (8 VGPRs per check),
+// each address formed per use (one add), with the words made opaque so the
+// compiler cannot hoist the 16 addresses back out of the loop.
+template <int KC, bool PACKED>
+struct FloodTab;
+template <int KC>
+struct FloodTab<KC, false> {
+  uint32_t pa[KC][8], ca[KC][8];
+  __device__ __forceinline__ void init(const uint32_t* ftab, int lane, uint32_t pbase, uint32_t cbase) {
+#pragma unroll
+    for (int i = 0; i < KC; ++i) {
+      uint32_t t[8];
+      load_row8(ftab + (size_t)(lane + 64 * i) * 8, t);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        pa[i][k] = pbase + (t[k] & 0xffffu);
+        ca[i][k] = cbase + (t[k] >> 16);
+      }
+    }
+  }
+  __device__ __forceinline__ void get(int i, uint32_t (&p)[8], uint32_t (&c)[8]) const {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      p[k] = pa[i][k];
+      c[k] = ca[i][k];
+    }
+  }
+};
+template <int KC>
+struct FloodTab<KC, true> {
+  uint32_t tr[KC][8], pb, cb;
+  __device__ __forceinline__ void init(const uint32_t* ftab, int lane, uint32_t pbase, uint32_t cbase) {
+    pb = pbase;
+    cb = cbase;
+#pragma unroll
+    for (int i = 0; i < KC; ++i) load_row8(ftab + (size_t)(lane + 64 * i) * 8, tr[i]);
+  }
+  __device__ __forceinline__ void get(int i, uint32_t (&p)[8], uint32_t (&c)[8]) const {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t t = opaque_always(tr[i][k]);
+      p[k] = pb + (t & 0xffffu);
+      c[k] = cb + (t >> 16);
+    }
+  }
+};
+
 struct FloodRuns {  // fblob header: runs of equal column degree (capi.cpp)
   int n_runs;
   int start[QLDPC_MAX_RUNS], count[QLDPC_MAX_RUNS], deg[QLDPC_MAX_RUNS], p0[QLDPC_MAX_RUNS];
@@ -802,21 +832,13 @@ ms_flood_kernel(DecodeArgs a) {
   const float* c2v_f = (const float*)c2v_b;
   const int m = a.m, n = a.n;
 
-  // static per-lane graph data: absolute LDS addresses (VGPRs for the kernel)
-  uint32_t pa[KC][8], ca[KC][8];
+  // static per-lane graph data (VGPRs for the kernel)
+  FloodTab<KC, QLDPC_FLOOD_PACKED> tab;
+  tab.init(ftab, lane, lds_addr(ws), lds_addr(ws) + (uint32_t)a.off_c2v);
   uint32_t livem = 0;
-  const uint32_t wbase = lds_addr(ws);
 #pragma unroll
-  for (int i = 0; i < KC; ++i) {
-    uint32_t t[8];
-    load_row8(ftab + (size_t)(lane + 64 * i) * 8, t);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      pa[i][k] = wbase + (t[k] & 0xffffu);
-      ca[i][k] = wbase + (uint32_t)a.off_c2v + (t[k] >> 16);
-    }
+  for (int i = 0; i < KC; ++i)
     if (lane + 64 * i < m) livem |= 1u << i;
-  }
   // the runs header lives in LDS (the first QLDPC_FLOOD_HDR bytes): one
   // broadcast read per field per iteration, no global latency in the loop
   const int n_runs = __builtin_amdgcn_readfirstlane(runs->n_runs);
@@ -849,19 +871,45 @@ ms_flood_kernel(DecodeArgs a) {
         for (int i = 0; i < KC; ++i) {
           const uint32_t negprod = ((neg * DC) ^ (synreg >> i)) & 1u;
           const uint32_t val = cb | ((neg ^ negprod) << 31);
+          uint32_t pa[8], ca[8];
+          tab.get(i, pa, ca);
 #pragma unroll
-          for (int k = 0; k < DC; ++k) *QLDPC_LDS(uint32_t, ca[i][k]) = val;
+          for (int k = 0; k < DC; ++k) *QLDPC_LDS(uint32_t, ca[k]) = val;
         }
       } else {
+#ifdef QLDPC_FLOOD_PIPE
+        // software pipeline: check i+1's LDS reads are in flight while check
+        // i computes (their edges are disjoint; post is read-only here)
+        CnLoad<DC> cur;
+        uint32_t pa[8], ca[8];
+        tab.get(0, pa, ca);
+        cn_ms_load<DC>(cur, pa, ca);
 #pragma unroll
         for (int i = 0; i < KC; ++i) {
-          const uint32_t live[1] = {(livem >> i) & 1u};
-          const uint32_t sb[1] = {(synreg >> i) & 1u};
-          unsat |= cn_ms_abs<DC>(a, pa[i], ca[i], sb[0], live[0], fl);
-#ifndef QLDPC_FLOOD_NOBAR
-          __builtin_amdgcn_sched_barrier(0);         // one check's working set at a time
-#endif
+          CnLoad<DC> nxt;
+          uint32_t pn[8], cn[8];
+          if (i + 1 < KC) {
+            tab.get(i + 1, pn, cn);
+            cn_ms_load<DC>(nxt, pn, cn);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          unsat |= cn_ms_compute<DC>(a, cur, ca, (synreg >> i) & 1u, (livem >> i) & 1u, fl);
+          __builtin_amdgcn_sched_barrier(0);
+          if (i + 1 < KC) {
+            cur = nxt;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) ca[k] = cn[k];
+          }
         }
+#else
+#pragma unroll
+        for (int i = 0; i < KC; ++i) {
+          uint32_t pa[8], ca[8];
+          tab.get(i, pa, ca);
+          unsat |= cn_ms_abs<DC>(a, pa, ca, (synreg >> i) & 1u, (livem >> i) & 1u, fl);
+          __builtin_amdgcn_sched_barrier(0);         // one check's working set at a time
+        }
+#endif
         // stop test of iteration it-1 (decoders.py:175-176)
         if (ballot(unsat != 0) == 0) {
           iters = it;
@@ -892,8 +940,10 @@ ms_flood_kernel(DecodeArgs a) {
 #pragma unroll
         for (int i = 0; i < KC; ++i) {
           uint32_t ph = 0;
+          uint32_t pa[8], ca[8];
+          tab.get(i, pa, ca);
 #pragma unroll
-          for (int k = 0; k < DC; ++k) ph ^= hi_word(*QLDPC_LDS(const double, pa[i][k]));
+          for (int k = 0; k < DC; ++k) ph ^= hi_word(*QLDPC_LDS(const double, pa[k]));
           un |= (((ph >> 31) ^ (synreg >> i)) & (livem >> i)) & 1u;
         }
         conv = ballot(un != 0) == 0;
