@@ -221,6 +221,11 @@ struct qldpc_schedule {
   int f_off_tab = 0;
   LaunchCfg cfg[2];           // per algo
   std::mutex mu;
+  // half-shot work-queue counters (ring: concurrent launches on different
+  // streams take different slots; each is zeroed on the launch stream)
+  static constexpr int kQueueSlots = 64;
+  uint32_t* d_queue = nullptr;
+  std::atomic<uint32_t> qnext{0};
 };
 
 static int align16(int x) { return (x + 15) & ~15; }
@@ -394,6 +399,7 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
     return QLDPC_OK;
   }
   hipError_t e1 = hipMalloc(&s->d_blob, s->blob.size());
+  if (e1 == hipSuccess) e1 = hipMalloc(&s->d_queue, sizeof(uint32_t) * qldpc_schedule::kQueueSlots);
   if (e1 == hipSuccess) e1 = hipMemcpy(s->d_blob, s->blob.data(), s->blob.size(), hipMemcpyHostToDevice);
   if (e1 == hipSuccess && !s->fblob.empty()) {
     e1 = hipMalloc(&s->d_fblob, s->fblob.size());
@@ -416,6 +422,7 @@ extern "C" int qldpc_schedule_destroy(qldpc_schedule* s) {
   (void)hipFree(s->d_blob);
   (void)hipFree(s->d_lblob);
   (void)hipFree(s->d_fblob);
+  (void)hipFree(s->d_queue);
   delete s;
   return QLDPC_OK;
 }
@@ -625,6 +632,10 @@ extern "C" int qldpc_decode_device(const qldpc_code* code, const qldpc_schedule*
   a.eps = eps;
   a.max_iter = max_iter;
 
+  a.queue = nullptr;
+  if (!getenv("QLDPC_STATIC_SCHED")) {
+    a.queue = sched->d_queue + (sched->qnext.fetch_add(1) % qldpc_schedule::kQueueSlots);
+  }
   int cus = 0;
   HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   const int64_t need = (batch + cfg->waves - 1) / cfg->waves;
@@ -632,6 +643,7 @@ extern "C" int qldpc_decode_device(const qldpc_code* code, const qldpc_schedule*
   const int grid = (int)std::max<int64_t>(1, std::min(need, resident));
   hipStream_t st = (hipStream_t)stream;
 
+  if (a.queue) HIP_TRY(hipMemsetAsync(a.queue, 0, sizeof(uint32_t), st));
   hipEvent_t e0 = nullptr, e1 = nullptr;
   bool timed;
   {

@@ -35,6 +35,7 @@ struct DecodeArgs {
   float L32;                  // float32(L)
   double beta, eps;
   int max_iter;
+  uint32_t* queue;            // half-shot work queue (zeroed before the launch), or null = static stride
 };
 
 const void* select_kernel(int algo, bool layered, int dc);

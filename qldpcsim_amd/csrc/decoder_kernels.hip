@@ -87,6 +87,45 @@ __device__ __forceinline__ void store_bits64(uint32_t* words, int c0, int pred, 
   if (lane == 1) words[(c0 >> 5) + 1] = (uint32_t)(b >> 32);
 }
 
+// Persistent half-shot loop. Each wave starts with one static half-shot;
+// with a queue, further work comes from a global ticket counter in guided
+// chunks (about remaining / (4 * waves) consecutive half-shots, at most 64,
+// at least 1), claimed with one atomic when the last half-shot of the current
+// chunk starts, so its latency is hidden. Early-terminating decodes (channel
+// syndromes: most stop after 1-3 iterations, a few run max_iter) then
+// balance across waves instead of leaving a long tail, and the counter sees
+// O(waves * log) atomics rather than one per half-shot.
+struct HalfShotQueue {
+  long long hs, end, stride, batch;
+  uint32_t* q;
+  uint32_t tk, tlen, seen;
+  __device__ __forceinline__ HalfShotQueue(const DecodeArgs& a, int waves, int wid)
+      : hs((long long)blockIdx.x * waves + wid), end(0), stride((long long)gridDim.x * waves),
+        batch(a.batch), q(a.queue), tk(0), tlen(1), seen(0) {
+    end = hs + 1;
+  }
+  __device__ __forceinline__ void prefetch(int lane) {
+    if (q && hs + 1 == end) {                       // last of this chunk: claim the next
+      const long long rem = batch - stride - (long long)seen;
+      long long len = rem / (4 * stride);
+      len = len < 1 ? 1 : (len > 64 ? 64 : len);
+      tlen = (uint32_t)len;
+      if (lane == 0) tk = atomicAdd(q, tlen);
+    }
+  }
+  __device__ __forceinline__ void advance() {
+    if (!q) {
+      hs += stride;
+      return;
+    }
+    if (++hs < end) return;
+    const uint32_t t = __builtin_amdgcn_readfirstlane(tk);
+    seen = t + tlen;
+    hs = stride + (long long)t;
+    end = hs + tlen;
+  }
+};
+
 struct LdsView {
   const uint32_t* cn_tab;   // [E] (relabeled var << 16) | csc position, CSR edge order
   const uint16_t* row_ptr;  // [m+1]
@@ -533,8 +572,9 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) decode_kernel(DecodeArgs a)
   const int m = a.m, n = a.n;
   const int nwords = (m + 31) >> 5;
 
-  for (long long hs = (long long)blockIdx.x * waves + wid; hs < a.batch;
-       hs += (long long)gridDim.x * waves) {
+  for (HalfShotQueue Q(a, waves, wid); Q.hs < a.batch; Q.advance()) {
+    const long long hs = Q.hs;
+    Q.prefetch(threadIdx.x & 63);
     const uint8_t* syn = a.syn + hs * (long long)m;
     int fl = 0;
     int iters = a.max_iter;
@@ -846,8 +886,9 @@ ms_flood_kernel(DecodeArgs a) {
   __syncthreads();
   const int* hdr = (const int*)lds;
 
-  for (long long hs = (long long)blockIdx.x * waves + wid; hs < a.batch;
-       hs += (long long)gridDim.x * waves) {
+  for (HalfShotQueue Q(a, waves, wid); Q.hs < a.batch; Q.advance()) {
+    const long long hs = Q.hs;
+    Q.prefetch(threadIdx.x & 63);
     const uint8_t* syn = a.syn + hs * (long long)m;
     int fl = 0;
     int iters = a.max_iter;
@@ -1005,8 +1046,9 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
   const int m = a.m, n = a.n;
   const int nwords = (m + 31) >> 5;
 
-  for (long long hs = (long long)blockIdx.x * waves + wid; hs < a.batch;
-       hs += (long long)gridDim.x * waves) {
+  for (HalfShotQueue Q(a, waves, wid); Q.hs < a.batch; Q.advance()) {
+    const long long hs = Q.hs;
+    Q.prefetch(threadIdx.x & 63);
     const uint8_t* syn = a.syn + hs * (long long)m;
     int fl = 0;
     int iters = a.max_iter;
