@@ -62,6 +62,26 @@ def pmc_traffic(code, batch):
     return None
 
 
+def onchip_profile(code):
+    """Unit utilisations of the decode kernel from the newest committed SQ
+    counter summary (profiles/*_counters.json, tools/ctr_summary.py --json):
+    the on-chip limiters of an LDS-resident kernel, which HBM bytes cannot show."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_counters.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get("code") == code:
+            keep = ("valu_busy", "lds_busy", "lds_conflict_share", "per_wave_iter_valu",
+                    "per_wave_iter_lds", "per_wave_iter_salu")
+            out = {k: round(d[k], 4) for k in keep if k in d}
+            out["source"] = os.path.relpath(path, ROOT)
+            return out
+    return None
+
+
 def cpu_baseline(code, max_iter, seconds, threads):
     """The pinned CPU oracle (oracle/qldpc_oracle.c, OpenMP over shots) timed on
     this host on a bounded sample of the same workload."""
@@ -181,9 +201,11 @@ def main():
             "note": "achieved = SURVEY 8d algorithmic bytes (4*(3E+2n) per executed half-shot "
                     "iteration + m+n+4 I/O) / mean decode-kernel duration (HIP events on the launch "
                     "stream). Message state is LDS-resident, so real HBM traffic (traffic) is "
-                    "far below the algorithmic model; the kernel's actual limiter is VALU/LDS.",
+                    "far below the algorithmic model; the kernel's actual limiters are on chip "
+                    "(onchip: VALU / LDS busy fractions from rocprofv3 SQ counters).",
             "kernel_ms_per_launch": avg_launch_s * 1e3,
             "launches": launches,
+            "onchip": onchip_profile(args.code),
         },
     }
     if world == 1 and rank == 0 and args.cpu_seconds > 0:
