@@ -131,9 +131,16 @@ def main():
     syn_x = torch.randint(0, 2, (B, Hx.shape[0]), dtype=torch.uint8, device=dev, generator=g)
     prior = 0.05 / 3
 
+    # output buffers allocated once (a step allocates nothing)
+    def buffers():
+        return decoders.DecodeResult(torch.empty((B, n), dtype=torch.uint8, device=dev),
+                                     torch.empty(B, dtype=torch.int32, device=dev), None,
+                                     torch.empty(B, dtype=torch.int32, device=dev))
+    out_z, out_x = buffers(), buffers()
+
     def step():
-        rz = decoders.decode_batch(Hz, syn_z, prior, args.iters, algo="MS")
-        rx = decoders.decode_batch(Hx, syn_x, prior, args.iters, algo="MS")
+        rz = decoders.decode_batch(Hz, syn_z, prior, args.iters, algo="MS", out=out_z)
+        rx = decoders.decode_batch(Hx, syn_x, prior, args.iters, algo="MS", out=out_x)
         return rz, rx
 
     for _ in range(args.warmup):

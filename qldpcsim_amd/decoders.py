@@ -52,13 +52,16 @@ def _is_torch(x):
 
 
 def decode_batch(H, syndromes, p, max_iter, layers=None, algo="MS", beta=0.75, eps=1e-9,
-                 want_post=False, osd_order=-1, layer_ptr=None, layer_rows=None, stream=None):
+                 want_post=False, osd_order=-1, layer_ptr=None, layer_rows=None, stream=None,
+                 out=None):
     """Decode a batch of syndromes of one matrix on the GPU.
 
     syndromes: uint8 [B, m] NumPy array (host; staged, synchronous) or a
     torch uint8 tensor on a HIP device (asynchronous on `stream` or torch's
     current stream; outputs are device tensors, OSD is not applied).
     `p` is the decoder prior (simulate passes p/3, simulator.py:278-282).
+    `out` (device path): a DecodeResult of matching device tensors to write
+    into instead of allocating (steady-state loops allocate nothing).
     """
     if algo not in _lib.ALGO:
         raise ValueError("Unrecognized decoder type.")
@@ -77,10 +80,22 @@ def decode_batch(H, syndromes, p, max_iter, layers=None, algo="MS", beta=0.75, e
         if syn.dtype != torch.uint8 or syn.dim() != 2 or syn.shape[1] != m:
             raise ValueError(f"syndromes must be uint8 [B, {m}]")
         B = syn.shape[0]
-        ehat = torch.empty((B, n), dtype=torch.uint8, device=dev)
-        iters = torch.empty(B, dtype=torch.int32, device=dev)
-        flags = torch.empty(B, dtype=torch.int32, device=dev)
-        post = torch.empty((B, n), dtype=torch.float64, device=dev) if want_post else None
+        if out is not None:
+            ehat, iters, flags, post = out.ehat, out.iters, out.flags, out.post if want_post else None
+            ok = (ehat.shape == (B, n) and ehat.dtype == torch.uint8 and iters.shape == (B,) and
+                  iters.dtype == torch.int32 and flags.shape == (B,) and flags.dtype == torch.int32 and
+                  all(t.device == dev and t.is_contiguous() for t in (ehat, iters, flags)) and
+                  (not want_post or (post is not None and post.shape == (B, n) and
+                                     post.dtype == torch.float64 and post.device == dev and
+                                     post.is_contiguous())))
+            if not ok:
+                raise ValueError("out buffers do not match the batch (uint8 [B, n], int32 [B], "
+                                 "int32 [B], float64 [B, n] if want_post) on the syndromes' device")
+        else:
+            ehat = torch.empty((B, n), dtype=torch.uint8, device=dev)
+            iters = torch.empty(B, dtype=torch.int32, device=dev)
+            flags = torch.empty(B, dtype=torch.int32, device=dev)
+            post = torch.empty((B, n), dtype=torch.float64, device=dev) if want_post else None
         st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
         _lib.check(_lib.lib.qldpc_decode_device(
             code.handle, sched.handle, _lib.ALGO[algo], syn.data_ptr(), B, float(p), int(max_iter),

@@ -169,3 +169,27 @@ def test_full_size_headline_batch_properties(dec):
     e, its, _, _ = oracle.decode_batch("MS", Hz, sub, 0.05 / 3, 50, want_post=False)
     np.testing.assert_array_equal(r1.ehat[torch.as_tensor(idx, device="cuda")].cpu().numpy(), e)
     np.testing.assert_array_equal(it[torch.as_tensor(idx, device="cuda")].cpu().numpy(), its)
+
+
+def test_decode_batch_into_preallocated_buffers(dec):
+    """decode_batch(out=...) writes the same results into caller buffers (the
+    bench's allocation-free steady state) and rejects mismatched buffers."""
+    import torch
+    from qldpcsim_amd import codes
+    Hx, Hz = codes.load_code("LP118_0")
+    B, n = 2048, Hz.shape[1]
+    g = torch.Generator(device="cuda").manual_seed(5)
+    syn = torch.randint(0, 2, (B, Hz.shape[0]), dtype=torch.uint8, device="cuda", generator=g)
+    ref = dec.decode_batch(Hz, syn, 0.05 / 3, 50, algo="MS", want_post=True)
+    out = dec.DecodeResult(torch.full((B, n), 7, dtype=torch.uint8, device="cuda"),
+                           torch.full((B,), -1, dtype=torch.int32, device="cuda"),
+                           torch.zeros((B, n), dtype=torch.float64, device="cuda"),
+                           torch.full((B,), -1, dtype=torch.int32, device="cuda"))
+    r = dec.decode_batch(Hz, syn, 0.05 / 3, 50, algo="MS", want_post=True, out=out)
+    torch.cuda.synchronize()
+    assert r.ehat.data_ptr() == out.ehat.data_ptr()
+    assert torch.equal(r.ehat, ref.ehat) and torch.equal(r.iters, ref.iters)
+    assert torch.equal(r.flags, ref.flags) and torch.equal(r.post, ref.post)
+    bad = dec.DecodeResult(out.ehat[:, :-1], out.iters, None, out.flags)
+    with pytest.raises(ValueError):
+        dec.decode_batch(Hz, syn, 0.05 / 3, 50, algo="MS", out=bad)
