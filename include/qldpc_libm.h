@@ -6,10 +6,12 @@
  * 1 - 1e-9): a one-ULP difference between two libms' tanh grows into ~1e-4
  * relative differences in converged posteriors. To make the GPU kernel and the
  * CPU oracle agree bit for bit, both evaluate these two functions with this
- * header: only IEEE-754 +, -, *, / (each correctly rounded on gfx950 and on
- * x86-64; compiled with -ffp-contract=off, no FMA), integer bit operations and
- * comparisons. Accuracy against NumPy's tanh/arctanh: <= 2 ULP over the BP
- * domain (tests/test_libm.py).
+ * header: only IEEE-754 +, -, *, / and explicit fused multiply-add (each
+ * correctly rounded on gfx950 — v_fma_f64 — and on x86-64 with FMA3; callers
+ * compile with -ffp-contract=off so no other contraction happens, and the
+ * host build needs -mfma so fma is the instruction, not glibc's emulation),
+ * integer bit operations and comparisons. Accuracy against NumPy's
+ * tanh/arctanh: <= 3 ULP over the BP domain (tests/test_libm.py).
  *
  * Method: tanh = e/(e+2), e = expm1(2|x|) (Cody–Waite reduction y = k ln2 + r,
  * |r| <= ln2/2, degree-14 Taylor polynomial, 2^k (1 + expm1 r) - 1
@@ -41,37 +43,40 @@ QLDPC_HD uint64_t qldpc_d2bits(double d) {
   return u;
 }
 
+#define QLDPC_FMA(a, b, c) __builtin_fma((a), (b), (c))
+
 #define QLDPC_LN2_HI 6.93147180369123816490e-01 /* 0x3fe62e42fee00000: k*LN2_HI exact for |k| < 2^11 */
 #define QLDPC_LN2_LO 1.90821492927058770002e-10 /* 0x3dea39ef35793c76 */
 #define QLDPC_INV_LN2 1.44269504088896338700e+00
 
-/* e^r - 1 for |r| <= ln2/2 (+ a little): r + r^2 * sum_{k>=2} r^(k-2)/k!  */
+/* e^r - 1 for |r| <= ln2/2 (+ a little): r + r^2 * sum_{k>=2} r^(k-2)/k!
+   (Horner with fused multiply-adds) */
 QLDPC_HD double qldpc_expm1_small(double r) {
-  double q = 1.0 / 87178291200.0;          /* 1/14! */
-  q = q * r + 1.0 / 6227020800.0;          /* 1/13! */
-  q = q * r + 1.0 / 479001600.0;           /* 1/12! */
-  q = q * r + 1.0 / 39916800.0;            /* 1/11! */
-  q = q * r + 1.0 / 3628800.0;             /* 1/10! */
-  q = q * r + 1.0 / 362880.0;              /* 1/9!  */
-  q = q * r + 1.0 / 40320.0;               /* 1/8!  */
-  q = q * r + 1.0 / 5040.0;                /* 1/7!  */
-  q = q * r + 1.0 / 720.0;                 /* 1/6!  */
-  q = q * r + 1.0 / 120.0;                 /* 1/5!  */
-  q = q * r + 1.0 / 24.0;                  /* 1/4!  */
-  q = q * r + 1.0 / 6.0;                   /* 1/3!  */
-  q = q * r + 0.5;                         /* 1/2!  */
-  return r + (r * r) * q;
+  double q = 1.0 / 87178291200.0;                 /* 1/14! */
+  q = QLDPC_FMA(q, r, 1.0 / 6227020800.0);        /* 1/13! */
+  q = QLDPC_FMA(q, r, 1.0 / 479001600.0);         /* 1/12! */
+  q = QLDPC_FMA(q, r, 1.0 / 39916800.0);          /* 1/11! */
+  q = QLDPC_FMA(q, r, 1.0 / 3628800.0);           /* 1/10! */
+  q = QLDPC_FMA(q, r, 1.0 / 362880.0);            /* 1/9!  */
+  q = QLDPC_FMA(q, r, 1.0 / 40320.0);             /* 1/8!  */
+  q = QLDPC_FMA(q, r, 1.0 / 5040.0);              /* 1/7!  */
+  q = QLDPC_FMA(q, r, 1.0 / 720.0);               /* 1/6!  */
+  q = QLDPC_FMA(q, r, 1.0 / 120.0);               /* 1/5!  */
+  q = QLDPC_FMA(q, r, 1.0 / 24.0);                /* 1/4!  */
+  q = QLDPC_FMA(q, r, 1.0 / 6.0);                 /* 1/3!  */
+  q = QLDPC_FMA(q, r, 0.5);                       /* 1/2!  */
+  return QLDPC_FMA(r * r, q, r);
 }
 
 /* e^y - 1 for 0 <= y <= 64 */
 QLDPC_HD double qldpc_expm1_pos(double y) {
   const int k = (int)(y * QLDPC_INV_LN2 + 0.5);
   const double fk = (double)k;
-  const double r = (y - fk * QLDPC_LN2_HI) - fk * QLDPC_LN2_LO;
+  const double r = QLDPC_FMA(-fk, QLDPC_LN2_LO, y - fk * QLDPC_LN2_HI);  /* fk*LN2_HI exact */
   const double em = qldpc_expm1_small(r);
   if (k == 0) return em;
   const double two_k = qldpc_bits2d((uint64_t)(k + 1023) << 52);
-  return (two_k - 1.0) + two_k * em;
+  return QLDPC_FMA(two_k, em, two_k - 1.0);      /* two_k - 1 exact for k <= 53 */
 }
 
 QLDPC_HD double qldpc_tanh(double x) {
@@ -119,9 +124,9 @@ QLDPC_HD double qldpc_log1p(double f) {
       const double cc = (k > 0) ? 1.0 - (u - f) : f - (u - 1.0);
       const double mu = qldpc_bits2d((ub & 0x000fffffffffffffull) | 0x3ff0000000000000ull);  /* [1,2) */
       double r = 1.4571067811865475 - 0.5 * mu;     /* |r - 1/mu| < 0.09 */
-      r = r * (2.0 - mu * r);
-      r = r * (2.0 - mu * r);
-      r = r * (2.0 - mu * r);
+      r = r * QLDPC_FMA(-mu, r, 2.0);
+      r = r * QLDPC_FMA(-mu, r, 2.0);
+      r = r * QLDPC_FMA(-mu, r, 2.0);
       const double two_mk = qldpc_bits2d((uint64_t)(1023 - ((int)((ub >> 52) & 0x7ff) - 1023)) << 52);
       c = cc * r * two_mk;
     }
@@ -129,21 +134,21 @@ QLDPC_HD double qldpc_log1p(double f) {
   const double s = fm / (2.0 + fm);
   const double z = s * s;
   double R = 2.0 / 25.0;
-  R = R * z + 2.0 / 23.0;
-  R = R * z + 2.0 / 21.0;
-  R = R * z + 2.0 / 19.0;
-  R = R * z + 2.0 / 17.0;
-  R = R * z + 2.0 / 15.0;
-  R = R * z + 2.0 / 13.0;
-  R = R * z + 2.0 / 11.0;
-  R = R * z + 2.0 / 9.0;
-  R = R * z + 2.0 / 7.0;
-  R = R * z + 2.0 / 5.0;
-  R = R * z + 2.0 / 3.0;
+  R = QLDPC_FMA(R, z, 2.0 / 23.0);
+  R = QLDPC_FMA(R, z, 2.0 / 21.0);
+  R = QLDPC_FMA(R, z, 2.0 / 19.0);
+  R = QLDPC_FMA(R, z, 2.0 / 17.0);
+  R = QLDPC_FMA(R, z, 2.0 / 15.0);
+  R = QLDPC_FMA(R, z, 2.0 / 13.0);
+  R = QLDPC_FMA(R, z, 2.0 / 11.0);
+  R = QLDPC_FMA(R, z, 2.0 / 9.0);
+  R = QLDPC_FMA(R, z, 2.0 / 7.0);
+  R = QLDPC_FMA(R, z, 2.0 / 5.0);
+  R = QLDPC_FMA(R, z, 2.0 / 3.0);
   R = R * z;
   const double hfsq = 0.5 * fm * fm;
   const double fk = (double)k;
-  return fk * QLDPC_LN2_HI + ((fm - (hfsq - s * (hfsq + R))) + (fk * QLDPC_LN2_LO + c));
+  return QLDPC_FMA(fk, QLDPC_LN2_HI, (fm - QLDPC_FMA(-s, hfsq + R, hfsq)) + QLDPC_FMA(fk, QLDPC_LN2_LO, c));
 }
 
 QLDPC_HD double qldpc_atanh(double x) {

@@ -45,7 +45,7 @@ def test_libm_bit_identical_gpu_vs_host(tmp_path):
     (tmp_path / "c.c").write_text(C_SRC)
     subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-fPIC", "-shared",
                     "-I", inc, "-o", str(tmp_path / "g.so"), str(tmp_path / "g.hip")], check=True)
-    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-fPIC", "-shared", "-I", inc, "-o",
+    subprocess.run(["gcc", "-O2", "-mfma", "-ffp-contract=off", "-fPIC", "-shared", "-I", inc, "-o",
                     str(tmp_path / "c.so"), str(tmp_path / "c.c")], check=True)
     rng = np.random.default_rng(0)
     x = np.concatenate([rng.uniform(-40, 40, 200000), rng.uniform(-1, 1, 200000),

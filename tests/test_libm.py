@@ -19,7 +19,7 @@ def probe(tmp_path_factory):
                    "void vt(const double*x,double*y,long n){for(long i=0;i<n;++i)y[i]=qldpc_tanh(x[i]);}\n"
                    "void va(const double*x,double*y,long n){for(long i=0;i<n;++i)y[i]=qldpc_atanh(x[i]);}\n")
     so = d / "probe.so"
-    subprocess.run(["gcc", "-O2", "-fPIC", "-ffp-contract=off", "-shared", "-I",
+    subprocess.run(["gcc", "-O2", "-mfma", "-fPIC", "-ffp-contract=off", "-shared", "-I",
                     os.path.join(ROOT, "include"), "-o", str(so), str(src)], check=True)
     return ctypes.CDLL(str(so))
 
