@@ -769,6 +769,9 @@ struct FloodTab<KC, false> {
       for (int k = 0; k < 8; ++k) {
         pa[i][k] = pbase + (t[k] & 0xffffu);
         ca[i][k] = cbase + (t[k] >> 16);
+        // opaque: otherwise the compiler keeps the packed words and re-forms
+        // one of the two addresses with a VALU add at every use
+        asm volatile("" : "+v"(pa[i][k]), "+v"(ca[i][k]));
       }
     }
   }
