@@ -290,9 +290,14 @@ __device__ __forceinline__ uint32_t cn_ms_compute(const DecodeArgs& a, const CnL
   min12_tree<DC>(v, min1, min2);
   const uint32_t ph = xor_tree<DC>(hp);                   // hard-decision parity (:174)
   const uint32_t sh = xor_tree<DC>(hv);                   // np.sign product (:157-159)
-  const double m1 = __builtin_isinf(min1) ? 0.0 : min1;   // (:165)
-  const double m2 = __builtin_isinf(min2) ? 0.0 : min2;   // (:166)
-  if (m1 == 0.0 && live) fl |= FLAG_MIN_ZERO;             // App. A.1.6 leak case (flagged)
+  double m1 = min1, m2 = min2;
+  // Rare cases behind one wave-uniform test: an infinite min (min2 = inf
+  // whenever min1 is) and a zero min (min1 = 0, App. A.1.6 leak case, flagged).
+  if (__builtin_expect(ballot((min1 == 0.0) | (min2 == __builtin_inf())) != 0, 0)) {
+    m1 = __builtin_isinf(min1) ? 0.0 : min1;              // (:165)
+    m2 = __builtin_isinf(min2) ? 0.0 : min2;              // (:166)
+    if (m1 == 0.0 && live) fl |= FLAG_MIN_ZERO;
+  }
   const uint32_t npm = ((sh >> 31) ^ synb) << 31;
   // c2v_e = fl32(beta * (|v_e| == min1 ? min2 : min1)), sign syn * prod *
   // sign_e (:167-168). The reference gives min2 to the first argmin only;
@@ -807,17 +812,23 @@ struct FloodRuns {  // fblob header: runs of equal column degree (capi.cpp)
   int start[QLDPC_MAX_RUNS], count[QLDPC_MAX_RUNS], deg[QLDPC_MAX_RUNS], p0[QLDPC_MAX_RUNS];
 };
 
+// Sequential float32 sum in ascending check order (np.sum axis=0). It starts
+// from the first term instead of 0.0f + x0: the two differ only in the sign of
+// an all-zero sum, and post = L + S is the same for S = +0 and S = -0 (L is
+// never -0), so the posteriors are bit-identical.
 template <int K>
 __device__ __forceinline__ float vn_sum(const float* c) {
-  float s = 0.0f;
-  if constexpr (K > 0) {
+  if constexpr (K == 0) {
+    return 0.0f;
+  } else {
     float x[K];
 #pragma unroll
     for (int t = 0; t < K; ++t) x[t] = c[t];
+    float s = x[0];
 #pragma unroll
-    for (int t = 0; t < K; ++t) s += x[t];               // float32, ascending check
+    for (int t = 1; t < K; ++t) s += x[t];               // float32, ascending check
+    return s;
   }
-  return s;
 }
 
 template <int K>
