@@ -32,7 +32,7 @@ from . import _lib
 from .schedule import pack_layers
 
 __all__ = ["MS_decoder", "BP_decoder", "OSDdec", "decode_batch", "DecodeResult", "osd_perm",
-           "osd_perms", "apply_osd", "apply_osd_device"]
+           "osd_perms", "apply_osd", "apply_osd_device", "apply_osd_device_many"]
 
 
 @dataclass
@@ -159,32 +159,73 @@ def osd_perms(post, nthreads=None):
         return np.concatenate(list(ex.map(one, np.array_split(post, 4 * nthreads))))
 
 
+_PINNED = {}
+
+
+def _pinned(key, shape, dtype):
+    """Grow-only page-locked host staging buffers (D2H of posteriors, H2D of
+    reliability orders run at DMA speed instead of through pageable copies)."""
+    import torch
+    need = int(np.prod(shape))
+    buf = _PINNED.get(key)
+    if buf is None or buf.numel() < need or buf.dtype != dtype:
+        buf = torch.empty(max(need, 1), dtype=dtype, pin_memory=True)
+        _PINNED[key] = buf
+    return buf[:need].view(*shape)
+
+
 def apply_osd_device(H, syn, res, order, stream=None):
     """GPU OSD (qldpc_osd_device) for the non-converged shots of a device
     decode `res` (DecodeResult of torch tensors, with posteriors): only their
-    posteriors travel to the host for NumPy's reliability order; the GF(2)
-    work runs on the GPU. Updates res.ehat in place."""
+    posteriors travel to the host (pinned, asynchronous) for NumPy's
+    reliability order; the GF(2) work runs on the GPU. Updates res.ehat in
+    place. See apply_osd_device_many for several decodes at once."""
+    return apply_osd_device_many([(H, syn, res)], order, stream)[0]
+
+
+def apply_osd_device_many(items, order, stream=None):
+    """apply_osd_device for several (H, syn, res) decodes (the X and Z halves
+    of a batch): every posterior copy is queued first, so the next copy runs
+    while the host computes the previous one's reliability order."""
     import torch
-    if res.post is None:
-        raise ValueError("apply_osd_device needs the decode's posteriors (want_post=True)")
-    bad = ((res.flags & _lib.FLAG_CONVERGED) == 0).nonzero().flatten()
-    k = int(bad.numel())
-    if k == 0:
-        return res.ehat
-    dev = res.ehat.device
-    code = _lib.code_for(H, dev.index)
-    perms = torch.as_tensor(osd_perms(res.post[bad].cpu().numpy()), device=dev)
-    syn_b = syn[bad].contiguous()
-    e_b = res.ehat[bad].contiguous()
-    status = torch.empty(k, dtype=torch.int32, device=dev)
-    st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
-    _lib.check(_lib.lib.qldpc_osd_device(code.handle, k, syn_b.data_ptr(), perms.data_ptr(), int(order),
-                                         e_b.data_ptr(), status.data_ptr(), st))
-    if bool((status != 0).any()):
-        # the reference's greedy basis loop indexes past column n-1 (decoders.py:333-342)
-        raise IndexError("OSD: column basis search ran past the last column")
-    res.ehat[bad] = e_b
-    return res.ehat
+    staged = []
+    for slot, (H, syn, res) in enumerate(items):
+        if res.post is None:
+            raise ValueError("apply_osd_device needs the decode's posteriors (want_post=True)")
+        dev = res.ehat.device
+        st = torch.cuda.current_stream(dev) if stream is None else stream
+        bad = ((res.flags & _lib.FLAG_CONVERGED) == 0).nonzero().flatten()
+        k = int(bad.numel())
+        if k == 0:
+            staged.append(None)
+            continue
+        host = _pinned(("post", slot), (k, res.post.shape[1]), torch.float64)
+        host.copy_(res.post.index_select(0, bad), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(st if isinstance(st, torch.cuda.Stream) else None)
+        staged.append((bad, host, ev))
+    for slot, ((H, syn, res), sg) in enumerate(zip(items, staged)):
+        if sg is None:
+            continue
+        bad, host, ev = sg
+        k = int(bad.numel())
+        dev = res.ehat.device
+        code = _lib.code_for(H, dev.index)
+        ev.synchronize()
+        perm_h = _pinned(("perm", slot), (k, host.shape[1]), torch.int32)
+        perm_h.numpy()[...] = osd_perms(host.numpy())
+        perms = perm_h.to(dev, non_blocking=True)
+        syn_b = syn.index_select(0, bad)
+        e_b = res.ehat.index_select(0, bad)
+        status = torch.empty(k, dtype=torch.int32, device=dev)
+        st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+        _lib.check(_lib.lib.qldpc_osd_device(code.handle, k, syn_b.data_ptr(), perms.data_ptr(), int(order),
+                                             e_b.data_ptr(), status.data_ptr(), st))
+        if bool((status != 0).any()):
+            # the reference's greedy basis loop indexes past column n-1 (decoders.py:333-342)
+            raise IndexError("OSD: column basis search ran past the last column")
+        res.ehat.index_copy_(0, bad, e_b)
+    return [r.ehat for _, _, r in items]
 
 
 def apply_osd(H, syn, ehat, post, flags, order, nthreads=0):

@@ -226,8 +226,7 @@ def simulate_p(Hx: np.ndarray, Hz: np.ndarray, p: float, shots: int = 1000, decT
             rZ = decoders.decode_batch(Hx, sy_x, p / 3, decIterations, algo=decType, want_post=want_post,
                                        layer_ptr=lpZ, layer_rows=lrZ)
             if osd >= 0:                               # (decoders.py:179-180), on the GPU
-                decoders.apply_osd_device(Hz, sy_z, rX, osd)
-                decoders.apply_osd_device(Hx, sy_x, rZ, osd)
+                decoders.apply_osd_device_many([(Hz, sy_z, rX), (Hx, sy_x, rZ)], osd)
             c = ch.count(sy_z, sy_x, errX, errZ, rX.ehat, rZ.ehat, rX.iters, rZ.iters)
         elif samples is not None:
             sl = slice(my_start + done, my_start + done + B)
