@@ -143,12 +143,16 @@ def main():
         rx = decoders.decode_batch(Hx, syn_x, prior, args.iters, algo="MS", out=out_x)
         return rz, rx
 
+    iters_sum = torch.zeros((), dtype=torch.int64, device=dev)
     for _ in range(args.warmup):
-        step()
+        # the same work as a timed step, including the iteration reduction (the
+        # first use of torch's reduce kernel loads its code object: ~0.1 s)
+        rz, rx = step()
+        iters_sum += rz.iters.sum(dtype=torch.int64) + rx.iters.sum(dtype=torch.int64)
     torch.cuda.synchronize()
     _lib.timing_enable(True)
     _lib.timing_reset()
-    iters_sum = torch.zeros((), dtype=torch.int64, device=dev)
+    iters_sum.zero_()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
