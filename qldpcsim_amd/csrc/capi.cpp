@@ -199,6 +199,7 @@ struct LaunchCfg {
   int waves = 0, blocks_per_cu = 0, lds = 0, wave_bytes = 0;
   bool lblob = false;  // uses the layer-ordered blob (ms_layered_kernel)
   bool gtab = false;     // ms_flood_kernel: global tables, LDS = wave state only
+  int team = 0;          // bp_team_kernel: waves per half-shot (one workgroup), 0 = wave kernels
   bool ok = false;
 };
 
@@ -441,6 +442,23 @@ static void wave_layout(const qldpc_code* c, bool layered, int algo, int* bytes,
   *bytes = std::max(off, 16);
 }
 
+// bp_team_kernel's slice: post f64[n] | c2v f64[E + 8] | syn words | parity
+// words | reduction slots ([2][W] any-flags, [2][2] tickets)
+static void team_layout(const qldpc_code* c, int w, int* bytes, int* off_c2v, int* off_synw,
+                        int* off_parw, int* off_red) {
+  int off = align16(8 * c->n);
+  *off_c2v = off;
+  off = align16(off + 8 * (c->E + 8));
+  const int words = 2 * ((c->m + 63) / 64);
+  *off_synw = off;
+  off = align16(off + 4 * words);
+  *off_parw = off;
+  off = align16(off + 4 * words);
+  *off_red = off;
+  off = align16(off + 4 * (2 * w + 4));
+  *bytes = off;
+}
+
 static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   std::lock_guard<std::mutex> lk(s->mu);
   LaunchCfg& cfg = s->cfg[algo];
@@ -466,15 +484,39 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   }
   cfg.lblob = use_lblob;
   cfg.gtab = gtab;
+  int team = 0;
+  if (!cfg.kernel && algo == QLDPC_ALGO_BP && dc > 0 && !getenv("QLDPC_BP_WAVE")) {
+    // 4 waves per half-shot; 8 when a team's LDS footprint leaves at most 3
+    // teams per CU (LP118_2: 67 KB), so a CU still runs >= 16 waves
+    int tb = 0, o1, o2, o3, o4;
+    team_layout(c, 4, &tb, &o1, &o2, &o3, &o4);
+    team = ((int)s->blob.size() + tb > 48 * 1024) ? 8 : 4;
+    if (const char* ev = getenv("QLDPC_BP_TEAM_W")) team = atoi(ev);
+    cfg.kernel = qldpc::select_bp_team_kernel(s->layered, dc, team);
+    if (!cfg.kernel) team = 0;
+  }
+  cfg.team = team;
   if (!cfg.kernel) cfg.kernel = qldpc::select_kernel(algo, s->layered, dc);
-  int off_c2v, off_synw, off_parw;
+  int off_c2v, off_synw, off_parw, off_red;
   wave_layout(c, s->layered, algo, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw);
+  if (team) team_layout(c, team, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw, &off_red);
   int max_lds = 0, dev = 0;
   HIP_TRY(hipGetDevice(&dev));
   HIP_TRY(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
   HIP_TRY(qldpc::configure_kernel(cfg.kernel, max_lds));
   const int blob = gtab ? QLDPC_FLOOD_HDR : (int)(use_lblob ? s->lblob.size() : s->blob.size());
   int best_waves = 0;
+  if (team) {  // one team (workgroup of `team` waves) per half-shot
+    const int lds = blob + cfg.wave_bytes;
+    int nb = 0;
+    if (lds <= max_lds)
+      HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cfg.kernel, 64 * team, (size_t)lds));
+    cfg.waves = team;
+    cfg.blocks_per_cu = nb;
+    cfg.lds = lds;
+    best_waves = nb * team;
+    max_waves = 0;  // skip the wave-kernel search below
+  }
   for (int w = max_waves; w >= 1; --w) {
     const int lds = blob + w * cfg.wave_bytes;
     if (lds > max_lds) continue;
@@ -488,7 +530,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
     }
   }
   // Tuning overrides (experiments only): QLDPC_WAVES_PER_WG, QLDPC_WG_PER_CU.
-  if (const char* ev = getenv("QLDPC_WAVES_PER_WG")) {
+  if (const char* ev = team ? nullptr : getenv("QLDPC_WAVES_PER_WG")) {
     const int w = atoi(ev);
     const int lds = blob + w * cfg.wave_bytes;
     int nb = 0;
@@ -609,6 +651,7 @@ extern "C" int qldpc_decode_device(const qldpc_code* code, const qldpc_schedule*
     a.off_chunk_dmax = sched->l_off_adj_dmax;
     a.off_vn_chk = sched->l_off_vn_chk;
   }
+  if (cfg->team) team_layout(code, cfg->team, &a.wave_bytes, &a.off_c2v, &a.off_synw, &a.off_parw, &a.off_red);
   if (cfg->gtab) {  // global tables; the LDS holds wave state only
     a.blob = sched->d_fblob;
     a.blob_bytes = 0;
@@ -638,7 +681,7 @@ extern "C" int qldpc_decode_device(const qldpc_code* code, const qldpc_schedule*
   }
   int cus = 0;
   HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  const int64_t need = (batch + cfg->waves - 1) / cfg->waves;
+  const int64_t need = cfg->team ? batch : (batch + cfg->waves - 1) / cfg->waves;
   const int64_t resident = (int64_t)cfg->blocks_per_cu * cus;
   const int grid = (int)std::max<int64_t>(1, std::min(need, resident));
   hipStream_t st = (hipStream_t)stream;

@@ -23,6 +23,7 @@ struct DecodeArgs {
   int off_lay_ptr, off_lay_rows, off_adj_ptr, off_adj_vars, off_chunk_dmax;
   int wave_bytes;             // per-wave state slice (multiple of 16)
   int off_c2v, off_synw, off_parw;  // inside a wave slice (post f64[n] at 0)
+  int off_red;                // bp_team_kernel: team reduction / ticket slots inside the team slice
   int m, n, E, n_layers;
   const uint16_t* vinv;       // [n] original column -> relabeled variable (global)
   const uint8_t* syn;         // [batch][m]
@@ -42,7 +43,9 @@ const void* select_kernel(int algo, bool layered, int dc);
 // flooding MS, uniform row degree: global tables (fblob), LDS = wave state only
 const void* select_ms_flood_kernel(int dc, int kc);  // nullptr if no instantiation fits
 int ms_flood_max_waves(int kc);                      // waves per workgroup it was compiled for
-const void* select_ms_layered_kernel(int dc);                // layered MS, uniform degree (blob: layer tables)                               // waves per workgroup it was compiled for
+const void* select_ms_layered_kernel(int dc);
+// BP, uniform row degree 7/8: one team of W waves per half-shot, edge-parallel check nodes
+const void* select_bp_team_kernel(bool layered, int dc, int w);                // layered MS, uniform degree (blob: layer tables)                               // waves per workgroup it was compiled for
 hipError_t launch_decode(const void* kernel, const DecodeArgs& args, int grid, int block,
                          int lds_bytes, hipStream_t stream);
 hipError_t configure_kernel(const void* kernel, int lds_bytes);

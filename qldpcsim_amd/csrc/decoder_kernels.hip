@@ -1139,6 +1139,237 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
 }
 
 // ---------------------------------------------------------------------------
+// Sum-product BP for uniform row degree DC (7 or 8): one TEAM of W wavefronts
+// (one workgroup) decodes one half-shot, with the check-node update spread
+// over the edges — 8 lanes per check, lane k owns edge k — instead of a lane
+// per check. Same arithmetic, same results as decode_kernel<BP, …, DC>, bit
+// for bit (decoders.py:249-262 per check):
+//   t_k  = tanh(v_k / 2)                 one lane per edge
+//   P    = ((t_0 t_1) t_2) ... t_{d-1}   np.prod's sequential fold, carried
+//                                        lane to lane by d-1 shuffles
+//   c2v_k = ±2 atanh(clip(P / t_k))       one lane per edge
+// Why: BP's float64 state is large (LP118_2: 37 KB per half-shot), so a
+// one-wave-per-half-shot kernel runs 3-7 waves per CU and stalls on the long
+// dependent tanh / atanh chains (30-60 % VALU busy). A team puts 4-8x the
+// lanes on one half-shot's state: more waves per CU for the same LDS, and a
+// layered layer (30-60 checks) becomes one pass of 8-lane groups.
+// Variable nodes: one lane per variable (np.sum pairwise rule), as before.
+// Team-wide stop tests go through LDS slots (double-buffered, one barrier).
+// ---------------------------------------------------------------------------
+template <int DC>
+__device__ __forceinline__ uint32_t cn_bp_group(const DecodeArgs& a, const LdsView& g, int c, bool valid,
+                                                int k, int lane, uint32_t synb, const double* post,
+                                                double* c2v, int& fl) {
+  const bool ek = valid && k < DC;
+  const uint32_t t = ek ? g.cn_tab[8 * c + k] : 0u;
+  const int j = (int)((t & 0xffffu) >> 3), p = (int)(t >> 18);
+  const double pj = ek ? post[j] : 0.0;
+  double th = 1.0;
+  if (ek) th = qldpc_tanh((pj - c2v[p]) / 2.0);           // v2c (:269), tanh (:254)
+  // np.prod: sequential left fold over the check's edges in ascending variable
+  // order; lane s multiplies the running product of lanes 0..s-1 by its t_s
+  double acc = th;
+#pragma unroll
+  for (int s = 1; s < DC; ++s) {
+    const double x = __shfl_up(acc, 1, 8);
+    if (k == s) acc = x * th;
+  }
+  const double P = __shfl(acc, (lane & ~7) + DC - 1, 64);
+  // parity of the hard decisions of the posteriors this check read (:283-285)
+  const uint64_t hb = ballot(ek && pj < 0.0);
+  const uint32_t par = (uint32_t)__builtin_popcount((uint32_t)(hb >> (lane & 56)) & 0xffu) & 1u;
+  if (ek) {
+    if (th == 0.0) fl |= FLAG_NONFINITE;
+    double th2 = P / th;                                  // (:256)
+    if (__builtin_fabs(th2) >= 1.0 - a.eps)               // (:257-258)
+      th2 = th2 - a.eps * (th2 > 0.0 ? 1.0 : (th2 < 0.0 ? -1.0 : 0.0));
+    double val = 2.0 * qldpc_atanh(th2);                  // (:259)
+    if (synb) val = -val;                                 // (:260-261)
+    if (!__builtin_isfinite(val)) fl |= FLAG_NONFINITE;
+    c2v[p] = val;
+  }
+  return valid ? (par ^ synb) : 0u;
+}
+
+template <bool LAYERED, int DC, int W>
+__global__ void __launch_bounds__(64 * W) bp_team_kernel(DecodeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  {
+    const uint4* src = (const uint4*)a.blob;
+    uint4* dst = (uint4*)lds;
+    const int nvec = a.blob_bytes >> 4;
+    for (int i = threadIdx.x; i < nvec; i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  LdsView g;
+  g.cn_tab = (const uint32_t*)(lds + a.off_cn_tab);
+  g.row_ptr = (const uint16_t*)(lds + a.off_row_ptr);
+  g.vn_info = (const uint32_t*)(lds + a.off_vn_ptr);
+  g.chunk_dmax = (const uint8_t*)(lds + a.off_chunk_dmax);
+  g.vn_chk = (const uint16_t*)(lds + a.off_vn_chk);
+  g.lay_ptr = (const uint16_t*)(lds + a.off_lay_ptr);
+  g.lay_rows = (const uint16_t*)(lds + a.off_lay_rows);
+  g.adj_ptr = (const uint16_t*)(lds + a.off_adj_ptr);
+  g.adj_vars = (const uint16_t*)(lds + a.off_adj_vars);
+
+  constexpr int TS = 64 * W;        // threads per team
+  constexpr int GP = 8 * W;         // 8-lane check groups per pass
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int grp = tid >> 3, k = tid & 7;
+  unsigned char* ws = lds + a.blob_bytes;
+  double* post = (double*)ws;
+  double* c2v = (double*)(ws + a.off_c2v);
+  uint32_t* synw = (uint32_t*)(ws + a.off_synw);
+  uint32_t* parw = (uint32_t*)(ws + a.off_parw);
+  uint32_t* red = (uint32_t*)(ws + a.off_red);          // [2][W] any-slots, [2][2] tickets
+  const int m = a.m, n = a.n;
+  const int nwords = (m + 31) >> 5;
+  const double L = a.L;
+
+  int rphase = 0;
+  auto team_any = [&](bool pred) -> bool {              // one barrier
+    const uint64_t b = ballot(pred);
+    if (lane == 0) red[rphase * W + wid] = b != 0;
+    __syncthreads();
+    bool r = false;
+#pragma unroll
+    for (int w = 0; w < W; ++w) r |= red[rphase * W + w] != 0;
+    rphase ^= 1;
+    return r;
+  };
+
+  // team-level guided work queue (HalfShotQueue's policy, one ticket per team)
+  long long hs = blockIdx.x, end = hs + 1;
+  const long long stride = gridDim.x;
+  uint32_t seen = 0, tlen = 1, tk = 0;
+  int tphase = 0;
+  while (hs < a.batch) {
+    bool claimed = false;
+    if (a.queue && hs + 1 == end) {
+      const long long rem = a.batch - stride - (long long)seen;
+      long long len = rem / (4 * stride);
+      len = len < 1 ? 1 : (len > 64 ? 64 : len);
+      tlen = (uint32_t)len;
+      claimed = true;
+      if (tid == 0) tk = atomicAdd(a.queue, tlen);
+    }
+    const uint8_t* syn = a.syn + hs * (long long)m;
+    int fl = 0;
+    int iters = a.max_iter;
+    bool conv = false;
+
+    // state: post = L, c2v = 0 (decoders.py:235-236); syndrome (and, layered,
+    // initial parity) bit-words
+    for (int j = tid; j < n; j += TS) post[j] = L;
+    for (int p = tid; p < a.E; p += TS) c2v[p] = 0.0;
+    for (int c0 = 64 * wid; c0 < m; c0 += TS) {
+      const int c = c0 + lane;
+      const int in = c < m;
+      store_bits64(synw, c0, in ? (syn[c] & 1) : 0, lane);
+      if constexpr (LAYERED) store_bits64(parw, c0, in && (L < 0.0) && (DC & 1), lane);
+    }
+    __syncthreads();
+
+    if constexpr (!LAYERED) {
+      for (int it = 0;; ++it) {
+        uint32_t unsat = 0;
+        for (int c0 = 0; c0 < m; c0 += GP) {
+          const int c = c0 + grp;
+          const bool valid = c < m;
+          const uint32_t sb = valid ? (synw[c >> 5] >> (c & 31)) & 1u : 0u;
+          unsat |= cn_bp_group<DC>(a, g, valid ? c : 0, valid, k, lane, sb, post, c2v, fl);
+        }
+        // the parity pass is the stop test of iteration it-1 (:283-285)
+        if (it > 0 && !team_any(unsat != 0)) {
+          iters = it;
+          conv = true;
+          break;
+        }
+        __syncthreads();
+        for (int j = tid; j < n; j += TS) post[j] = vn_post<ALGO_BP>(a, g, j, c2v, -1);
+        __syncthreads();
+        if (it + 1 == a.max_iter) {
+          uint32_t un = 0;
+          for (int c = tid; c < m; c += TS) {
+            uint32_t par = 0;
+#pragma unroll
+            for (int q = 0; q < DC; ++q) par ^= (uint32_t)(post[tab_var<DC>(g.cn_tab[8 * c + q])] < 0.0);
+            un |= par ^ ((synw[c >> 5] >> (c & 31)) & 1u);
+          }
+          conv = !team_any(un != 0);
+          break;
+        }
+      }
+    } else {
+      for (int it = 0; it < a.max_iter && !conv; ++it) {
+        for (int l = 0; l < a.n_layers; ++l) {
+          const int q0 = g.lay_ptr[l], q1 = g.lay_ptr[l + 1];
+          for (int qb = q0; qb < q1; qb += GP) {
+            const int q = qb + grp;
+            const bool valid = q < q1;
+            const int c = valid ? (int)g.lay_rows[q] : 0;
+            const uint32_t sb = valid ? (synw[c >> 5] >> (c & 31)) & 1u : 0u;
+            (void)cn_bp_group<DC>(a, g, c, valid, k, lane, sb, post, c2v, fl);
+          }
+          __syncthreads();
+          // VN over the layer's adjacent variables; flips toggle check parities
+          const int v0 = g.adj_ptr[l], v1 = g.adj_ptr[l + 1];
+          for (int q = v0 + tid; q < v1; q += TS) {
+            const int j = g.adj_vars[q];
+            const double old = post[j];
+            const double nw = vn_post<ALGO_BP>(a, g, j, c2v, -1);
+            post[j] = nw;
+            if ((old < 0.0) != (nw < 0.0)) {
+              const uint32_t info = g.vn_info[j];
+              for (int p = (int)(info & 0xffffu), pe = p + (int)(info >> 16); p < pe; ++p) {
+                const int c = g.vn_chk[p];
+                atomicXor(&parw[c >> 5], 1u << (c & 31));
+              }
+            }
+          }
+          __syncthreads();
+          uint32_t un = 0;                               // stop test after every layer (:283-285)
+          for (int w = tid; w < nwords; w += TS) un |= parw[w] ^ synw[w];
+          if (!team_any(un != 0)) {
+            iters = it + 1;
+            conv = true;
+            break;
+          }
+        }
+      }
+    }
+
+    uint8_t* eh = a.ehat + hs * (long long)n;
+    double* po = a.post ? a.post + hs * (long long)n : nullptr;
+    for (int jo = tid; jo < n; jo += TS) {
+      const double pv = post[a.vinv[jo]];
+      eh[jo] = (uint8_t)(pv < 0.0);                       // (:280)
+      if (po) po[jo] = pv;
+    }
+    const bool nonfin = team_any((fl & FLAG_NONFINITE) != 0);
+    if (tid == 0) {
+      a.iters[hs] = iters;
+      if (a.flags) a.flags[hs] = (int32_t)((nonfin ? FLAG_NONFINITE : 0) | (conv ? FLAG_CONVERGED : 0));
+      if (claimed) {
+        red[2 * W + 2 * tphase] = tk;
+        red[2 * W + 2 * tphase + 1] = tlen;
+      }
+    }
+    __syncthreads();                                      // slice reuse; ticket visible
+    if (!a.queue) {
+      hs += stride;
+    } else if (++hs >= end) {
+      const uint32_t t0 = red[2 * W + 2 * tphase], l0 = red[2 * W + 2 * tphase + 1];
+      tphase ^= 1;
+      seen = t0 + l0;
+      hs = stride + (long long)t0;
+      end = hs + l0;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Host-side launch helpers (called from capi.cpp)
 // ---------------------------------------------------------------------------
 template <int ALGO, bool LAYERED, int DC>
@@ -1156,6 +1387,14 @@ const void* select_ms_flood_kernel(int dc, int kc) {
   if (dc == 8 && kc <= 4) return (const void*)&ms_flood_kernel<8, 4>;
   if (dc == 7 && kc <= 8) return (const void*)&ms_flood_kernel<7, 8>;
   if (dc == 8 && kc <= 8) return (const void*)&ms_flood_kernel<8, 8>;
+  return nullptr;
+}
+
+const void* select_bp_team_kernel(bool layered, int dc, int w) {
+#define QLDPC_BPT(L, D, Wn) if (layered == L && dc == D && w == Wn) return (const void*)&bp_team_kernel<L, D, Wn>;
+  QLDPC_BPT(false, 7, 4) QLDPC_BPT(false, 8, 4) QLDPC_BPT(true, 7, 4) QLDPC_BPT(true, 8, 4)
+  QLDPC_BPT(false, 7, 8) QLDPC_BPT(false, 8, 8) QLDPC_BPT(true, 7, 8) QLDPC_BPT(true, 8, 8)
+#undef QLDPC_BPT
   return nullptr;
 }
 
