@@ -85,15 +85,16 @@ __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
     inJ[0] = 1;
   }
   nJ = 1;
+  // Fully unrolled over the NW words, so every R[w] / R[q] index is a
+  // compile-time constant and the row stays in VGPRs (a runtime word index
+  // would put R in scratch memory: one global access per touch).
+#pragma unroll
   for (int w = 0; w < NW; ++w) {
-    if (done || 64 * w >= n) break;
+    if (done || 64 * w >= n) continue;
     for (int b = 0; b < 64; ++b) {
       const int i = 64 * w + b;
       if (i >= n || done) break;
-      uint64_t cur = 0;                             // R[w] without a runtime register index
-#pragma unroll
-      for (int q = 0; q < NW; ++q) cur = (q == w) ? R[q] : cur;
-      const bool has = own && ((cur >> b) & 1ull);
+      const bool has = own && ((R[w] >> b) & 1ull);
       const uint64_t bal = __ballot(has && t >= xrow);
       int* sl = slots + 16 * (step & 1);
       if (lane == 0) sl[wave] = bal ? wave * 64 + __builtin_ctzll(bal) : 0x7fffffff;
@@ -106,7 +107,7 @@ __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
       // other row holding a 1 in column i is XOR-ed with it (below and above)
       if (t == piv) {
 #pragma unroll
-        for (int q = 0; q < NW; ++q) pivbuf[q] = R[q];
+        for (int q = w; q < NW; ++q) pivbuf[q] = R[q];  // the pivot row is 0 left of word w
       }
       if (t == xrow && piv != xrow) {
 #pragma unroll
@@ -118,11 +119,10 @@ __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
         for (int q = 0; q < NW; ++q) R[q] = swapbuf[q];   // old row xrow: 0 in column i
       } else if (t == xrow) {
 #pragma unroll
-        for (int q = 0; q < NW; ++q) R[q] = pivbuf[q];
+        for (int q = 0; q < NW; ++q) R[q] = q < w ? 0ull : pivbuf[q];
       } else if (has) {
 #pragma unroll
-        for (int q = 0; q < NW; ++q)
-          if (q >= w) R[q] ^= pivbuf[q];                 // pivot row is 0 left of column i
+        for (int q = w; q < NW; ++q) R[q] ^= pivbuf[q];  // pivot row is 0 left of column i
       }
       if (i != 0) {
         if (t == 0) {
