@@ -148,18 +148,8 @@ __device__ __forceinline__ int tab_var(uint32_t t) { return DC ? (int)((t & 0xff
 template <int DC>
 __device__ __forceinline__ int tab_pos(uint32_t t) { return DC ? (int)(t >> 18) : (int)(t & 0xffffu); }
 
-// Hide a register value's provenance from the optimizer: values derived from
-// it (addresses, predicates) are then recomputed where used instead of being
-// hoisted out of the persistent loop, which would cost one VGPR each.
-template <int WHICH>  // 1: check-node table words, 2: variable-node words
-__device__ __forceinline__ uint32_t opaque(uint32_t x) {
-#ifndef QLDPC_OPAQUE_MASK
-#define QLDPC_OPAQUE_MASK 2  // hoist check-node addresses (measured fastest), recompute VN ones
-#endif
-  if constexpr ((QLDPC_OPAQUE_MASK & WHICH) != 0) asm volatile("" : "+v"(x));
-  return x;
-}
-
+// Hide a register value's provenance from the optimizer, so that values
+// derived from it are not re-derived (or hoisted) where that costs VALU or VGPRs.
 __device__ __forceinline__ uint32_t opaque_always(uint32_t x) {
   asm volatile("" : "+v"(x));
   return x;
@@ -753,17 +743,10 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) decode_kernel(DecodeArgs a)
 //    p0 + o * K): no per-variable table, no masking, a compile-time K.
 // The LDS then holds only wave state: post f64[n] | c2v f32[E + 8].
 // ---------------------------------------------------------------------------
-#ifndef QLDPC_FLOOD_PACKED
-#define QLDPC_FLOOD_PACKED false
-#endif
-// Per-lane edge addresses of the KC checks a lane owns. Absolute: 16 VGPRs
-// per check, no VALU per use. Packed: the table words (8 VGPRs per check),
-// each address formed per use (one add), with the words made opaque so the
-// compiler cannot hoist the 16 addresses back out of the loop.
-template <int KC, bool PACKED>
-struct FloodTab;
+// Per-lane edge addresses of the KC checks a lane owns: absolute LDS byte
+// addresses, 16 VGPRs per check, no VALU per use.
 template <int KC>
-struct FloodTab<KC, false> {
+struct FloodTab {
   uint32_t pa[KC][8], ca[KC][8];
   __device__ __forceinline__ void init(const uint32_t* ftab, int lane, uint32_t pbase, uint32_t cbase) {
 #pragma unroll
@@ -788,25 +771,6 @@ struct FloodTab<KC, false> {
     }
   }
 };
-template <int KC>
-struct FloodTab<KC, true> {
-  uint32_t tr[KC][8], pb, cb;
-  __device__ __forceinline__ void init(const uint32_t* ftab, int lane, uint32_t pbase, uint32_t cbase) {
-    pb = pbase;
-    cb = cbase;
-#pragma unroll
-    for (int i = 0; i < KC; ++i) load_row8(ftab + (size_t)(lane + 64 * i) * 8, tr[i]);
-  }
-  __device__ __forceinline__ void get(int i, uint32_t (&p)[8], uint32_t (&c)[8]) const {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const uint32_t t = opaque_always(tr[i][k]);
-      p[k] = pb + (t & 0xffffu);
-      c[k] = cb + (t >> 16);
-    }
-  }
-};
-
 struct FloodRuns {  // fblob header: runs of equal column degree (capi.cpp)
   int n_runs;
   int start[QLDPC_MAX_RUNS], count[QLDPC_MAX_RUNS], deg[QLDPC_MAX_RUNS], p0[QLDPC_MAX_RUNS];
@@ -887,7 +851,7 @@ ms_flood_kernel(DecodeArgs a) {
   const int m = a.m, n = a.n;
 
   // static per-lane graph data (VGPRs for the kernel)
-  FloodTab<KC, QLDPC_FLOOD_PACKED> tab;
+  FloodTab<KC> tab;
   tab.init(ftab, lane, lds_addr(ws), lds_addr(ws) + (uint32_t)a.off_c2v);
   uint32_t livem = 0;
 #pragma unroll
@@ -932,31 +896,6 @@ ms_flood_kernel(DecodeArgs a) {
           for (int k = 0; k < DC; ++k) *QLDPC_LDS(uint32_t, ca[k]) = val;
         }
       } else {
-#ifdef QLDPC_FLOOD_PIPE
-        // software pipeline: check i+1's LDS reads are in flight while check
-        // i computes (their edges are disjoint; post is read-only here)
-        CnLoad<DC> cur;
-        uint32_t pa[8], ca[8];
-        tab.get(0, pa, ca);
-        cn_ms_load<DC>(cur, pa, ca);
-#pragma unroll
-        for (int i = 0; i < KC; ++i) {
-          CnLoad<DC> nxt;
-          uint32_t pn[8], cn[8];
-          if (i + 1 < KC) {
-            tab.get(i + 1, pn, cn);
-            cn_ms_load<DC>(nxt, pn, cn);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-          unsat |= cn_ms_compute<DC>(a, cur, ca, (synreg >> i) & 1u, (livem >> i) & 1u, fl);
-          __builtin_amdgcn_sched_barrier(0);
-          if (i + 1 < KC) {
-            cur = nxt;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) ca[k] = cn[k];
-          }
-        }
-#else
 #pragma unroll
         for (int i = 0; i < KC; ++i) {
           uint32_t pa[8], ca[8];
@@ -964,7 +903,6 @@ ms_flood_kernel(DecodeArgs a) {
           unsat |= cn_ms_abs<DC>(a, pa, ca, (synreg >> i) & 1u, (livem >> i) & 1u, fl);
           __builtin_amdgcn_sched_barrier(0);         // one check's working set at a time
         }
-#endif
         // stop test of iteration it-1 (decoders.py:175-176)
         if (ballot(unsat != 0) == 0) {
           iters = it;
