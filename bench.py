@@ -114,11 +114,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    # one process per GPU; QLDPC_BENCH_BACKEND=gloo (and more ranks than GPUs,
+    # ranks sharing a device) only to exercise this path on a one-GPU box
+    backend = os.environ.get("QLDPC_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from qldpcsim_amd import _lib, codes, decoders
     Hx, Hz = codes.load_code(args.code)
