@@ -32,7 +32,8 @@ from . import _lib
 from .schedule import pack_layers
 
 __all__ = ["MS_decoder", "BP_decoder", "OSDdec", "decode_batch", "DecodeResult", "osd_perm",
-           "osd_perms", "apply_osd", "apply_osd_device", "apply_osd_device_many"]
+           "osd_perms", "apply_osd", "apply_osd_device", "apply_osd_device_many", "osd_device_stage",
+           "osd_device_finish", "osd_status_check"]
 
 
 @dataclass
@@ -169,7 +170,10 @@ def _pinned(key, shape, dtype):
     need = int(np.prod(shape))
     buf = _PINNED.get(key)
     if buf is None or buf.numel() < need or buf.dtype != dtype:
-        buf = torch.empty(max(need, 1), dtype=dtype, pin_memory=True)
+        # page-locking is slow (ms per call): grow geometrically, start at 1 MiB
+        old = 0 if buf is None or buf.dtype != dtype else buf.numel()
+        cap = max(need, 2 * old, (1 << 20) // torch.empty((), dtype=dtype).element_size())
+        buf = torch.empty(cap, dtype=dtype, pin_memory=True)
         _PINNED[key] = buf
     return buf[:need].view(*shape)
 
@@ -187,27 +191,45 @@ def apply_osd_device_many(items, order, stream=None):
     """apply_osd_device for several (H, syn, res) decodes (the X and Z halves
     of a batch): every posterior copy is queued first, so the next copy runs
     while the host computes the previous one's reliability order."""
+    staged = osd_device_stage(items, stream)
+    osd_device_finish(items, staged, order, stream)
+    osd_status_check(items)
+    return [r.ehat for _, _, r in items]
+
+
+def osd_device_stage(items, stream=None, slot0=0):
+    """First half of the device OSD: find each decode's non-converged shots
+    (one device sync) and queue the asynchronous copy of their posteriors into
+    pinned host buffers. Returns the staging records for osd_device_finish.
+    `slot0` selects the pinned buffer set (pipelined callers alternate)."""
     import torch
     staged = []
     for slot, (H, syn, res) in enumerate(items):
         if res.post is None:
             raise ValueError("apply_osd_device needs the decode's posteriors (want_post=True)")
         dev = res.ehat.device
-        st = torch.cuda.current_stream(dev) if stream is None else stream
         bad = ((res.flags & _lib.FLAG_CONVERGED) == 0).nonzero().flatten()
         k = int(bad.numel())
         if k == 0:
             staged.append(None)
             continue
-        host = _pinned(("post", slot), (k, res.post.shape[1]), torch.float64)
+        host = _pinned(("post", slot0 + slot), (k, res.post.shape[1]), torch.float64)
         host.copy_(res.post.index_select(0, bad), non_blocking=True)
         ev = torch.cuda.Event()
-        ev.record(st if isinstance(st, torch.cuda.Stream) else None)
-        staged.append((bad, host, ev))
-    for slot, ((H, syn, res), sg) in enumerate(zip(items, staged)):
+        ev.record(torch.cuda.current_stream(dev))
+        staged.append((bad, host, ev, slot0 + slot))
+    return staged
+
+
+def osd_device_finish(items, staged, order, stream=None):
+    """Second half: NumPy's reliability order on the host for each staged
+    decode (waiting only for its own copy), then the GPU elimination and the
+    scatter of the corrected estimates, all queued asynchronously."""
+    import torch
+    for (H, syn, res), sg in zip(items, staged):
         if sg is None:
             continue
-        bad, host, ev = sg
+        bad, host, ev, slot = sg
         k = int(bad.numel())
         dev = res.ehat.device
         code = _lib.code_for(H, dev.index)
@@ -221,11 +243,18 @@ def apply_osd_device_many(items, order, stream=None):
         st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
         _lib.check(_lib.lib.qldpc_osd_device(code.handle, k, syn_b.data_ptr(), perms.data_ptr(), int(order),
                                              e_b.data_ptr(), status.data_ptr(), st))
-        if bool((status != 0).any()):
-            # the reference's greedy basis loop indexes past column n-1 (decoders.py:333-342)
-            raise IndexError("OSD: column basis search ran past the last column")
         res.ehat.index_copy_(0, bad, e_b)
-    return [r.ehat for _, _, r in items]
+        res.osd_status = status      # checked by the caller (raises IndexError like the reference)
+    return staged
+
+
+def osd_status_check(items):
+    """Raise the reference's IndexError if any OSD of these decodes ran its
+    greedy basis loop past the last column (decoders.py:333-342)."""
+    for _, _, res in items:
+        st = getattr(res, "osd_status", None)
+        if st is not None and bool((st != 0).any()):
+            raise IndexError("OSD: column basis search ran past the last column")
 
 
 def apply_osd(H, syn, ehat, post, flags, order, nthreads=0):

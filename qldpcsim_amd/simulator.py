@@ -139,7 +139,8 @@ class DeviceChannel:
     def _syn(e, HT):
         return (e.half() @ HT).to(dtype=e.dtype) & 1
 
-    def count(self, sy_z, sy_x, errX, errZ, eX, eZ, itX, itZ):
+    def count_device(self, sy_z, sy_x, errX, errZ, eX, eZ, itX, itZ):
+        """The six counters as an int64 device tensor (no host sync)."""
         torch = self.torch
         exact = (errX == eX).all(dim=1) & (errZ == eZ).all(dim=1)
         # integer products (no mod 2), as simulator.py:296
@@ -148,8 +149,11 @@ class DeviceChannel:
         degen = (~exact) & zX & zZ
         failX = (self._syn(eX, self.HzT) != sy_z).any(dim=1)
         failZ = (self._syn(eZ, self.HxT) != sy_x).any(dim=1)
-        v = torch.stack([failX.sum(), failZ.sum(), exact.sum(), degen.sum(),
-                         itX.to(torch.int64).sum(), itZ.to(torch.int64).sum()]).cpu().tolist()
+        return torch.stack([failX.sum(), failZ.sum(), exact.sum(), degen.sum(),
+                            itX.to(torch.int64).sum(), itZ.to(torch.int64).sum()])
+
+    def count(self, sy_z, sy_x, errX, errZ, eX, eZ, itX, itZ):
+        v = self.count_device(sy_z, sy_x, errX, errZ, eX, eZ, itX, itZ).cpu().tolist()
         return dict(zip(COUNTER_KEYS, (int(x) for x in v)))
 
 
@@ -216,29 +220,54 @@ def simulate_p(Hx: np.ndarray, Hz: np.ndarray, p: float, shots: int = 1000, decT
         import torch
         dev = torch.device("cuda", torch.cuda.current_device())
         ch = DeviceChannel(Hx, Hz, dev, np.random.SeedSequence(seed).generate_state(1, np.uint64)[0])
-    while done < my_shots:
+    if use_dev:
+        # Two-stage pipeline over batches: the host computes batch b-1's OSD
+        # reliability orders (NumPy) while the GPU samples and decodes batch b;
+        # counters accumulate on the device (one sync per batch, in the OSD
+        # staging; none without OSD until the end).
+        acc = torch.zeros(len(COUNTER_KEYS), dtype=torch.int64, device=dev)
+        pending = None
+        phase = 0
+        while done < my_shots or pending is not None:
+            cur = None
+            if done < my_shots:
+                B = min(batch_size, my_shots - done)
+                sy_z, sy_x, errX, errZ = ch.sample(p, B)
+                want_post = osd >= 0
+                rX = decoders.decode_batch(Hz, sy_z, p / 3, decIterations, algo=decType, want_post=want_post,
+                                           layer_ptr=lpX, layer_rows=lrX)
+                rZ = decoders.decode_batch(Hx, sy_x, p / 3, decIterations, algo=decType, want_post=want_post,
+                                           layer_ptr=lpZ, layer_rows=lrZ)
+                cur = [sy_z, sy_x, errX, errZ, rX, rZ, None]
+                done += B
+            if pending is not None:
+                sy_z_, sy_x_, errX_, errZ_, rX_, rZ_, staged = pending
+                items = [(Hz, sy_z_, rX_), (Hx, sy_x_, rZ_)]
+                if osd >= 0:                           # (decoders.py:179-180), on the GPU
+                    decoders.osd_device_finish(items, staged, osd)
+                    decoders.osd_status_check(items)
+                acc += ch.count_device(sy_z_, sy_x_, errX_, errZ_, rX_.ehat, rZ_.ehat, rX_.iters, rZ_.iters)
+            if cur is not None and osd >= 0:
+                cur[6] = decoders.osd_device_stage([(Hz, cur[0], cur[4]), (Hx, cur[1], cur[5])],
+                                                   slot0=2 * phase)
+                phase ^= 1
+            pending = cur
+            if verbose and rank == 0 and cur is not None:
+                print(f"\r(p={p:5.2e}) Decoding block n. {done:3}/{my_shots:4}... "
+                      f"({done / (time.time() - t0):.3g} shots/s)", end="", flush=True)
+        tot = dict(zip(COUNTER_KEYS, (int(x) for x in acc.cpu().tolist())))
+    while not use_dev and done < my_shots:
         B = min(batch_size, my_shots - done)
-        if use_dev:
-            sy_z, sy_x, errX, errZ = ch.sample(p, B)
-            want_post = osd >= 0
-            rX = decoders.decode_batch(Hz, sy_z, p / 3, decIterations, algo=decType, want_post=want_post,
-                                       layer_ptr=lpX, layer_rows=lrX)
-            rZ = decoders.decode_batch(Hx, sy_x, p / 3, decIterations, algo=decType, want_post=want_post,
-                                       layer_ptr=lpZ, layer_rows=lrZ)
-            if osd >= 0:                               # (decoders.py:179-180), on the GPU
-                decoders.apply_osd_device_many([(Hz, sy_z, rX), (Hx, sy_x, rZ)], osd)
-            c = ch.count(sy_z, sy_x, errX, errZ, rX.ehat, rZ.ehat, rX.iters, rZ.iters)
-        elif samples is not None:
+        if samples is not None:
             sl = slice(my_start + done, my_start + done + B)
             sy_z, sy_x, errX, errZ = (np.asarray(a)[sl].astype(np.uint8) for a in samples)
         else:
             sy_z, sy_x, errX, errZ = sample_channel(Hx, Hz, p, B, rng)
-        if not use_dev:
-            rX = decoders.decode_batch(Hz, sy_z, p / 3, decIterations, algo=decType, osd_order=osd,
-                                       layer_ptr=lpX, layer_rows=lrX)
-            rZ = decoders.decode_batch(Hx, sy_x, p / 3, decIterations, algo=decType, osd_order=osd,
-                                       layer_ptr=lpZ, layer_rows=lrZ)
-            c = count_outcomes(Hx, Hz, sy_z, sy_x, errX, errZ, rX.ehat, rZ.ehat, rX.iters, rZ.iters)
+        rX = decoders.decode_batch(Hz, sy_z, p / 3, decIterations, algo=decType, osd_order=osd,
+                                   layer_ptr=lpX, layer_rows=lrX)
+        rZ = decoders.decode_batch(Hx, sy_x, p / 3, decIterations, algo=decType, osd_order=osd,
+                                   layer_ptr=lpZ, layer_rows=lrZ)
+        c = count_outcomes(Hx, Hz, sy_z, sy_x, errX, errZ, rX.ehat, rZ.ehat, rX.iters, rZ.iters)
         for k in tot:
             tot[k] += c[k]
         done += B

@@ -107,6 +107,9 @@ def _channel(Hx, Hz, p, B, seed):
     ("LP118_0", "F", "BP", None, 5, 512),         # short horizon: every posterior within tolerance
     ("LP118_0", "L", "BP", None, 3, 256),
     ("LP118_0", "L", "MS", 0.05, 50, 2048),
+    ("LP118_2", "L", "BP", 0.08, 100, 128),       # BP team kernel, 8 waves per half-shot
+    ("LP118_2", "F", "BP", None, 4, 128),
+    ("LP04_0", "F", "BP", 0.1, 100, 512),         # BP team kernel, row degree 7
     ("LP118_0", "S", "MS", 0.05, 3, 256),
     ("T", "F", "MS", 0.05, 50, 1024),
 ])
