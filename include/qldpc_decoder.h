@@ -136,6 +136,42 @@ int qldpc_osd_device(const qldpc_code *code, int64_t count, const uint8_t *d_syn
  * (the reference's infoSet[0], decoders.py:344); -1 if empty. */
 int qldpc_cpython_setdiff_first(int n, const int32_t *J, int nJ);
 
+/* ---- Monte-Carlo shot source and counters on the device -----------------
+ * Replace simulate_p's shot source and per-shot bookkeeping
+ * (simulator.py:196-197 Stim sample, :249-252 row slicing, :291-303 outcome
+ * counting) so that a batch never leaves HBM. hx / hz are the two codes of
+ * the pair (same n), created on the current device.
+ *
+ * qldpc_channel_thresholds: the 32-bit draw thresholds of the depolarizing
+ * channel, T_k = floor(k * (p/3) * 2^32) (k = 1, 2, 3); p outside [0, 1]
+ * -> QLDPC_EINVAL (reference: assert at simulator.py:332).
+ *
+ * qldpc_channel_sample: shots shot0 .. shot0+batch-1 of the stream `seed`.
+ * Per qubit j of shot s: u = Philox4x32-10(key = seed, counter = (j % 64,
+ * (j / 64) / 4, s mod 2^32, s >> 32))[(j / 64) % 4]; X if u < T1, Y if
+ * T1 <= u < T2, Z if T2 <= u < T3 (PAULI_CHANNEL_1(p/3,p/3,p/3),
+ * simulator.py:107); errX = X|Y, errZ = Z|Y; sy_z = Hz errX mod 2,
+ * sy_x = Hx errZ mod 2 (the circuit's detector layout, :249-252).
+ *   d_errx, d_errz  uint64 [batch][ceil(n/64)]  bit j%64 of word j/64
+ *   d_syn_z uint8 [batch][m_z],  d_syn_x uint8 [batch][m_x]
+ *
+ * qldpc_count_outcomes: adds this batch's outcomes to d_counters int64[6] =
+ * {DecFailures_X, DecFailures_Z, decSuccessExact, decSuccessDegen,
+ *  sum of iterations X, sum of iterations Z} with the reference's exact
+ * definitions (simulator.py:291-303; "degen" is the integer, not mod-2,
+ * product of :296-298). d_ehat_x: uint8 [batch][n] estimate of errX (the
+ * decode of Hz / sy_z); d_ehat_z: estimate of errZ (Hx / sy_x); d_iters_*
+ * int32 [batch]. Asynchronous on `stream`, no host synchronisation. */
+int qldpc_channel_thresholds(double p, uint64_t *t1, uint64_t *t2, uint64_t *t3);
+int qldpc_channel_sample(const qldpc_code *hx, const qldpc_code *hz, double p, uint64_t seed,
+                         uint64_t shot0, int64_t batch, uint64_t *d_errx, uint64_t *d_errz,
+                         uint8_t *d_syn_z, uint8_t *d_syn_x, void *stream);
+int qldpc_count_outcomes(const qldpc_code *hx, const qldpc_code *hz, int64_t batch,
+                         const uint64_t *d_errx, const uint64_t *d_errz, const uint8_t *d_syn_z,
+                         const uint8_t *d_syn_x, const uint8_t *d_ehat_x, const uint8_t *d_ehat_z,
+                         const int32_t *d_iters_x, const int32_t *d_iters_z, int64_t *d_counters,
+                         void *stream);
+
 /* Kernel timing (HIP events around each decode kernel launch, on the launch
  * stream). Enabled by qldpc_timing_enable(1); qldpc_timing_read returns the
  * summed kernel milliseconds and launch count since the last reset. */

@@ -31,6 +31,10 @@ def lib():
                                           ctypes.c_int, ctypes.c_double, ctypes.c_double,
                                           P, P, P, P, ctypes.c_int]
         L.oracle_decode_batch.restype = ctypes.c_int
+        U64 = ctypes.c_uint64
+        L.oracle_channel_sample.argtypes = [ctypes.c_int, ctypes.c_int, P, P, ctypes.c_int, P, P,
+                                            U64, U64, U64, U64, U64, ctypes.c_long, P, P, P, P]
+        L.oracle_channel_sample.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -181,3 +185,29 @@ def osd_dec(H, e_hat, syndrome, post, order=0):
         ep[J] = ((T.astype(np.int64) @ sJ) % 2)[:len(J)]
     e_hat[perm] = ep
     return e_hat
+
+
+def channel_thresholds(p):
+    """T_k = floor(k * (p/3) * 2^32), k = 1, 2, 3 (qldpc_channel_thresholds)."""
+    q = p / 3.0
+    return tuple(int(min(2.0 ** 32, np.floor((k + 1) * q * 2.0 ** 32))) for k in range(3))
+
+
+def channel_sample(Hx, Hz, p, seed, shot0, batch):
+    """Restatement of the device sampler stream (qldpc_channel_sample).
+
+    Returns (sy_z, sy_x, errX, errZ) uint8 arrays, unpacked."""
+    Hx = np.asarray(Hx)
+    Hz = np.asarray(Hz)
+    n = Hx.shape[1]
+    rpx, cix = csr(Hx)
+    rpz, ciz = csr(Hz)
+    t1, t2, t3 = channel_thresholds(p)
+    ex = np.zeros((batch, n), np.uint8)
+    ez = np.zeros((batch, n), np.uint8)
+    syz = np.zeros((batch, Hz.shape[0]), np.uint8)
+    syx = np.zeros((batch, Hx.shape[0]), np.uint8)
+    lib().oracle_channel_sample(n, Hx.shape[0], _p(rpx), _p(cix), Hz.shape[0], _p(rpz), _p(ciz),
+                                t1, t2, t3, int(seed) & (2 ** 64 - 1), int(shot0), int(batch),
+                                _p(ex), _p(ez), _p(syz), _p(syx))
+    return syz, syx, ex, ez

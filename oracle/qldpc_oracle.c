@@ -256,3 +256,60 @@ int oracle_decode_batch(int algo, int m, int n, const int32_t *row_ptr, const in
     graph_free(&g);
     return rc;
 }
+
+/* ------------------------------------------------------------------------
+ * Channel sampler restatement (checker for qldpc_channel_sample,
+ * channel_kernels.hip). The shot source it replaces is the reference's Stim
+ * circuit sample (simulator.py:107 PAULI_CHANNEL_1(p/3,p/3,p/3) on every data
+ * qubit, :196-197 sampling, :249-252 row slicing); this stream is its
+ * statistical equivalent, so parity is defined on the
+ * stream itself: Philox4x32-10 as published by Salmon, Moraes, Dror and
+ * Shaw, "Parallel random numbers: as easy as 1, 2, 3" (SC'11), round
+ * multipliers 0xD2511F53 / 0xCD9E8D57, Weyl key increments 0x9E3779B9 /
+ * 0xBB67AE85. Outputs are unpacked bytes (errX, errZ uint8 [B][n]). */
+static void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    c[1] = (uint32_t)p1;
+    c[3] = (uint32_t)p0;
+    c[0] = n0;
+    c[2] = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+int oracle_channel_sample(int n, int mx, const int32_t *rpx, const int32_t *cix, int mz,
+                          const int32_t *rpz, const int32_t *ciz, uint64_t t1, uint64_t t2,
+                          uint64_t t3, uint64_t seed, uint64_t shot0, long batch, uint8_t *errx,
+                          uint8_t *errz, uint8_t *syz, uint8_t *syx) {
+  for (long b = 0; b < batch; ++b) {
+    const uint64_t s = shot0 + (uint64_t)b;
+    uint8_t *ex = errx + b * (long)n, *ez = errz + b * (long)n;
+    for (int j = 0; j < n; ++j) {
+      const int w = j / 64;
+      uint32_t c[4] = {(uint32_t)(j % 64), (uint32_t)(w / 4), (uint32_t)s, (uint32_t)(s >> 32)};
+      philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+      const uint64_t u = c[w % 4];
+      ex[j] = u < t2;                 /* X or Y */
+      ez[j] = u >= t1 && u < t3;      /* Y or Z */
+    }
+    for (int r = 0; r < mz; ++r) {
+      int par = 0;
+      for (int e = rpz[r]; e < rpz[r + 1]; ++e) par ^= ex[ciz[e]];
+      syz[b * (long)mz + r] = (uint8_t)par;
+    }
+    for (int r = 0; r < mx; ++r) {
+      int par = 0;
+      for (int e = rpx[r]; e < rpx[r + 1]; ++e) par ^= ez[cix[e]];
+      syx[b * (long)mx + r] = (uint8_t)par;
+    }
+  }
+  return 0;
+}
+
+/* raw block function, for the published known-answer vectors (tests) */
+void oracle_philox4x32_10(uint32_t *ctr, uint32_t k0, uint32_t k1) { philox4x32_10(ctr, k0, k1); }

@@ -24,6 +24,7 @@ EXPORTS = (
     "qldpc_schedule_create", "qldpc_schedule_destroy",
     "qldpc_decode_device", "qldpc_decode_host",
     "qldpc_osd_decode", "qldpc_osd_decode_batch", "qldpc_osd_device", "qldpc_cpython_setdiff_first",
+    "qldpc_channel_thresholds", "qldpc_channel_sample", "qldpc_count_outcomes",
     "qldpc_timing_enable", "qldpc_timing_reset", "qldpc_timing_read",
 )
 
@@ -64,6 +65,9 @@ def _load():
         "qldpc_osd_decode_batch": ([P, I64, P, P, I, P, I], I),
         "qldpc_osd_device": ([P, I64, P, P, I, P, P, P], I),
         "qldpc_cpython_setdiff_first": ([I, P, I], I),
+        "qldpc_channel_thresholds": ([D, P, P, P], I),
+        "qldpc_channel_sample": ([P, P, D, ctypes.c_uint64, ctypes.c_uint64, I64, P, P, P, P, P], I),
+        "qldpc_count_outcomes": ([P, P, I64, P, P, P, P, P, P, P, P, P, P], I),
         "qldpc_timing_enable": ([I], I),
         "qldpc_timing_reset": ([], I),
         "qldpc_timing_read": ([P, P], I),

@@ -25,6 +25,7 @@
 #include "../../include/qldpc_decoder.h"
 #include "decoder_kernels.h"
 #include "osd_kernels.h"
+#include "channel_kernels.h"
 
 using qldpc::DecodeArgs;
 
@@ -1063,5 +1064,108 @@ extern "C" int qldpc_osd_device(const qldpc_code* code, int64_t count, const uin
     HIP_TRY(hipLaunchKernel(k, dim3((unsigned)g), dim3(block), params, (size_t)lds, (hipStream_t)stream));
     done += g;
   }
+  return QLDPC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// device channel sampler and outcome counters (channel_kernels.hip)
+// ---------------------------------------------------------------------------
+static int pair_tabs(const qldpc_code* hx, const qldpc_code* hz, qldpc::PairTabs* t) {
+  if (!hx || !hz) return fail(QLDPC_EINVAL, "code is null");
+  if (hx->n != hz->n)
+    return fail(QLDPC_EINVAL, "Hx and Hz must have the same number of columns (physical qubits).");
+  if (hx->device < 0 || hz->device < 0)
+    return fail(QLDPC_EHIP, "no HIP device was visible when the code was created");
+  if (hx->device != hz->device) return fail(QLDPC_EINVAL, "Hx and Hz live on different devices");
+  const int W = (hx->n + 63) / 64;
+  if (W > 64) return fail(QLDPC_EUNSUP, "the channel kernels support n <= 4096 qubits (got %d)", hx->n);
+  t->rp_x = hx->d_row_ptr;
+  t->ci_x = hx->d_col_idx;
+  t->rp_z = hz->d_row_ptr;
+  t->ci_z = hz->d_col_idx;
+  t->mx = hx->m;
+  t->mz = hz->m;
+  t->ex = hx->E;
+  t->ez = hz->E;
+  t->n = hx->n;
+  t->W = W;
+  t->udeg = (hx->uniform_deg == hz->uniform_deg && hx->m > 0 && hz->m > 0) ? hx->uniform_deg : 0;
+  int dev = 0, max_lds = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  HIP_TRY(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
+  if (qldpc::channel_lds_bytes(*t, true) > max_lds)
+    return fail(QLDPC_EUNSUP, "the channel kernels need %d B of LDS for these codes",
+                qldpc::channel_lds_bytes(*t, true));
+  return QLDPC_OK;
+}
+
+static int channel_grid(int64_t batch) {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  const int64_t need = (batch + qldpc::kChannelWaves - 1) / qldpc::kChannelWaves;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(need, (int64_t)cus * 8));
+}
+
+extern "C" int qldpc_channel_thresholds(double p, uint64_t* t1, uint64_t* t2, uint64_t* t3) {
+  if (!(p >= 0.0 && p <= 1.0)) return fail(QLDPC_EINVAL, "p must lie in [0, 1] (got %g)", p);
+  const double q = p / 3.0, two32 = 4294967296.0;
+  uint64_t t[3];
+  for (int k = 0; k < 3; ++k) t[k] = (uint64_t)std::min(two32, std::floor((k + 1) * q * two32));
+  if (t1) *t1 = t[0];
+  if (t2) *t2 = t[1];
+  if (t3) *t3 = t[2];
+  return QLDPC_OK;
+}
+
+extern "C" int qldpc_channel_sample(const qldpc_code* hx, const qldpc_code* hz, double p, uint64_t seed,
+                                    uint64_t shot0, int64_t batch, uint64_t* d_errx, uint64_t* d_errz,
+                                    uint8_t* d_syn_z, uint8_t* d_syn_x, void* stream) {
+  qldpc::SampleArgs a{};
+  int rc = pair_tabs(hx, hz, &a.t);
+  if (rc != QLDPC_OK) return rc;
+  if (batch < 0) return fail(QLDPC_EINVAL, "negative batch");
+  rc = qldpc_channel_thresholds(p, &a.t1, &a.t2, &a.t3);
+  if (rc != QLDPC_OK) return rc;
+  if (batch == 0) return QLDPC_OK;
+  if (!d_errx || !d_errz || (a.t.mz && !d_syn_z) || (a.t.mx && !d_syn_x))
+    return fail(QLDPC_EINVAL, "null device buffer");
+  a.errx = d_errx;
+  a.errz = d_errz;
+  a.syz = d_syn_z;
+  a.syx = d_syn_x;
+  a.batch = batch;
+  a.shot0 = shot0;
+  a.key0 = (uint32_t)seed;
+  a.key1 = (uint32_t)(seed >> 32);
+  HIP_TRY(qldpc::launch_channel_sample(a, channel_grid(batch), (hipStream_t)stream));
+  return QLDPC_OK;
+}
+
+extern "C" int qldpc_count_outcomes(const qldpc_code* hx, const qldpc_code* hz, int64_t batch,
+                                    const uint64_t* d_errx, const uint64_t* d_errz, const uint8_t* d_syn_z,
+                                    const uint8_t* d_syn_x, const uint8_t* d_ehat_x, const uint8_t* d_ehat_z,
+                                    const int32_t* d_iters_x, const int32_t* d_iters_z, int64_t* d_counters,
+                                    void* stream) {
+  qldpc::CountArgs a{};
+  int rc = pair_tabs(hx, hz, &a.t);
+  if (rc != QLDPC_OK) return rc;
+  if (batch < 0) return fail(QLDPC_EINVAL, "negative batch");
+  if (batch == 0) return QLDPC_OK;
+  if (!d_errx || !d_errz || (a.t.mz && !d_syn_z) || (a.t.mx && !d_syn_x) || !d_ehat_x || !d_ehat_z ||
+      !d_iters_x || !d_iters_z || !d_counters)
+    return fail(QLDPC_EINVAL, "null device buffer");
+  a.errx = d_errx;
+  a.errz = d_errz;
+  a.syz = d_syn_z;
+  a.syx = d_syn_x;
+  a.ehx = d_ehat_x;
+  a.ehz = d_ehat_z;
+  a.itx = d_iters_x;
+  a.itz = d_iters_z;
+  a.acc = reinterpret_cast<unsigned long long*>(d_counters);
+  a.batch = batch;
+  HIP_TRY(qldpc::launch_count_outcomes(a, channel_grid(batch), (hipStream_t)stream));
   return QLDPC_OK;
 }

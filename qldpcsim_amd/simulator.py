@@ -19,7 +19,9 @@ counters are summed with one all_reduce (RCCL over xGMI on the GPU node).
 Syndrome source: Stim is not available in this environment,
 so shots come from a per-qubit Pauli sampler (X, Y, Z each p/3 — the
 circuit's PAULI_CHANNEL_1(p/3,p/3,p/3), simulator.py:107) whose statistics
-equal the circuit's. `rngSeed` seeds it (the reference
+equal the circuit's: on the GPU a counter-based Philox
+stream drawn by a HIP kernel next to the outcome counters (DeviceChannel,
+channel_kernels.hip); on the host NumPy's generator (sample_channel). `rngSeed` seeds it (the reference
 seeds np.random, which its unseeded Stim sampler never reads: runs there are
 not reproducible; here they are).
 """
@@ -30,7 +32,7 @@ from typing import Optional
 
 import numpy as np
 
-from . import decoders
+from . import _lib, decoders
 from .schedule import layerize, select_layers, pack_layers  # noqa: F401  (re-exported)
 
 __all__ = ["load_matrix", "simulate_p", "simulate", "main", "layerize", "sample_channel",
@@ -106,51 +108,67 @@ def count_outcomes(Hx, Hz, sy_z, sy_x, errX, errZ, eX, eZ, itX, itZ):
 
 
 class DeviceChannel:
-    """Device-side depolarizing sampler and outcome counters (torch on the HIP
-    device): the same per-qubit draw as `sample_channel` and the same counter
-    definitions as `count_outcomes`, without moving shots through host memory.
-    Syndromes are H·e mod 2 from an fp16 GEMM (exact: at most row-weight
-    nonzero products per entry)."""
+    """Device-side shot source and outcome counters (channel_kernels.hip via
+    the C ABI): the depolarizing draw of `sample_channel` as a counter-based
+    Philox stream (qldpc_channel_sample: shot s of seed k is the same whatever
+    the batching) and the counter definitions of `count_outcomes`
+    (qldpc_count_outcomes), so a batch never leaves HBM.
 
-    def __init__(self, Hx, Hz, device, seed):
+    sample() returns (sy_z uint8 [B, m_z], sy_x uint8 [B, m_x], errX, errZ)
+    with errX / errZ bit-packed as int64 [B, ceil(n/64)] words (bit j % 64 of
+    word j / 64); `unpack` turns them into uint8 [B, n]."""
+
+    def __init__(self, Hx, Hz, device, seed, shot0=0):
         import torch
         self.torch = torch
-        self.dev = device
-        self.HxT = torch.as_tensor(Hx.T, dtype=torch.half, device=device).contiguous()
-        self.HzT = torch.as_tensor(Hz.T, dtype=torch.half, device=device).contiguous()
+        self.dev = torch.device(device)
         self.n = Hx.shape[1]
-        self.gen = torch.Generator(device=device)
-        self.gen.manual_seed(int(seed) & ((1 << 63) - 1))
+        self.W = (self.n + 63) // 64
+        with torch.cuda.device(self.dev):
+            self.cx = _lib.code_for(Hx, self.dev.index)
+            self.cz = _lib.code_for(Hz, self.dev.index)
+        self.mx, self.mz = self.cx.m, self.cz.m
+        self.seed = int(seed) & ((1 << 64) - 1)
+        self.shot = int(shot0)
+
+    def _stream(self):
+        return self.torch.cuda.current_stream(self.dev).cuda_stream
 
     def sample(self, p, B):
         torch = self.torch
-        u = torch.rand((B, self.n), device=self.dev, generator=self.gen)
-        q = p / 3
-        X = u < q
-        Y = (u >= q) & (u < 2 * q)
-        Z = (u >= 2 * q) & (u < p)
-        errX = (X | Y).to(torch.uint8)
-        errZ = (Z | Y).to(torch.uint8)
-        sy_z = self._syn(errX, self.HzT)
-        sy_x = self._syn(errZ, self.HxT)
+        errX = torch.empty((B, self.W), dtype=torch.int64, device=self.dev)
+        errZ = torch.empty((B, self.W), dtype=torch.int64, device=self.dev)
+        sy_z = torch.empty((B, self.mz), dtype=torch.uint8, device=self.dev)
+        sy_x = torch.empty((B, self.mx), dtype=torch.uint8, device=self.dev)
+        _lib.check(_lib.lib.qldpc_channel_sample(
+            self.cx.handle, self.cz.handle, float(p), self.seed, self.shot, int(B), errX.data_ptr(),
+            errZ.data_ptr(), sy_z.data_ptr(), sy_x.data_ptr(), self._stream()))
+        self.shot += int(B)
         return sy_z, sy_x, errX, errZ
 
-    @staticmethod
-    def _syn(e, HT):
-        return (e.half() @ HT).to(dtype=e.dtype) & 1
-
-    def count_device(self, sy_z, sy_x, errX, errZ, eX, eZ, itX, itZ):
-        """The six counters as an int64 device tensor (no host sync)."""
+    def unpack(self, words):
+        """Packed int64 [B, W] error words -> uint8 [B, n] (device)."""
         torch = self.torch
-        exact = (errX == eX).all(dim=1) & (errZ == eZ).all(dim=1)
-        # integer products (no mod 2), as simulator.py:296
-        zX = ((errX ^ eX).half() @ self.HzT == 0).all(dim=1)
-        zZ = ((errZ ^ eZ).half() @ self.HxT == 0).all(dim=1)
-        degen = (~exact) & zX & zZ
-        failX = (self._syn(eX, self.HzT) != sy_z).any(dim=1)
-        failZ = (self._syn(eZ, self.HxT) != sy_x).any(dim=1)
-        return torch.stack([failX.sum(), failZ.sum(), exact.sum(), degen.sum(),
-                            itX.to(torch.int64).sum(), itZ.to(torch.int64).sum()])
+        bits = torch.arange(64, device=words.device, dtype=torch.int64)
+        return ((words.unsqueeze(-1) >> bits) & 1).to(torch.uint8).reshape(words.shape[0], -1)[:, :self.n]
+
+    def count_device(self, sy_z, sy_x, errX, errZ, eX, eZ, itX, itZ, acc=None):
+        """Adds the batch's six counters (COUNTER_KEYS order) to `acc`
+        (int64 [6] device tensor, created if None) without a host sync."""
+        torch = self.torch
+        if acc is None:
+            acc = torch.zeros(len(COUNTER_KEYS), dtype=torch.int64, device=self.dev)
+        B = sy_z.shape[0]
+        ts = (sy_z, sy_x, errX, errZ, eX, eZ, itX, itZ)
+        if not all(t.is_contiguous() and t.device == self.dev for t in ts) or \
+                eX.shape != (B, self.n) or eZ.shape != (B, self.n) or errX.shape != (B, self.W) or \
+                eX.dtype != torch.uint8 or itX.dtype != torch.int32 or itZ.dtype != torch.int32:
+            raise ValueError("count_device: buffers do not match the batch layout")
+        _lib.check(_lib.lib.qldpc_count_outcomes(
+            self.cx.handle, self.cz.handle, int(B), errX.data_ptr(), errZ.data_ptr(), sy_z.data_ptr(),
+            sy_x.data_ptr(), eX.data_ptr(), eZ.data_ptr(), itX.data_ptr(), itZ.data_ptr(),
+            acc.data_ptr(), self._stream()))
+        return acc
 
     def count(self, sy_z, sy_x, errX, errZ, eX, eZ, itX, itZ):
         v = self.count_device(sy_z, sy_x, errX, errZ, eX, eZ, itX, itZ).cpu().tolist()
@@ -177,13 +195,13 @@ def _dist():
 
 def simulate_p(Hx: np.ndarray, Hz: np.ndarray, p: float, shots: int = 1000, decType: str = "MS",
                decIterations: int = 99, decSchedule: str = "F", OSDorder: int = -1,
-               rngSeed: Optional[int] = None, *, batch_size: int = 1 << 16,
+               rngSeed: Optional[int] = None, *, batch_size: Optional[int] = None,
                verbose: bool = True, samples=None, sampler: Optional[str] = None) -> dict:
     """One depolarizing probability: sample, decode both halves, count.
 
     Returns the reference's dict (simulator.py:308-315). `samples`, if given,
     is a tuple (sy_z, sy_x, errX, errZ) to decode instead of sampling (used by
-    the parity tests). `sampler`: "device" (torch RNG + counters on the GPU,
+    the parity tests). `sampler`: "device" (HIP sampler + counters on the GPU,
     the default when a device is present), or "host" (NumPy). Extra keyword
     arguments default to reference behaviour.
     """
@@ -216,6 +234,8 @@ def simulate_p(Hx: np.ndarray, Hz: np.ndarray, p: float, shots: int = 1000, decT
     t0 = time.time()
     done = 0
     use_dev = sampler == "device" or (sampler is None and samples is None and _device_ok())
+    if batch_size is None:       # shots per batch: HBM holds 2^18-shot batches easily
+        batch_size = (1 << 18) if use_dev else (1 << 16)
     if use_dev:
         import torch
         dev = torch.device("cuda", torch.cuda.current_device())
@@ -246,7 +266,7 @@ def simulate_p(Hx: np.ndarray, Hz: np.ndarray, p: float, shots: int = 1000, decT
                 if osd >= 0:                           # (decoders.py:179-180), on the GPU
                     decoders.osd_device_finish(items, staged, osd)
                     decoders.osd_status_check(items)
-                acc += ch.count_device(sy_z_, sy_x_, errX_, errZ_, rX_.ehat, rZ_.ehat, rX_.iters, rZ_.iters)
+                ch.count_device(sy_z_, sy_x_, errX_, errZ_, rX_.ehat, rZ_.ehat, rX_.iters, rZ_.iters, acc)
             if cur is not None and osd >= 0:
                 cur[6] = decoders.osd_device_stage([(Hz, cur[0], cur[4]), (Hx, cur[1], cur[5])],
                                                    slot0=2 * phase)
@@ -310,7 +330,7 @@ def format_results(p, results, shots):
 
 def simulate(HxFile: str, HzFile: str, p, shots: int = 1000, decType: str = "MS",
              decIterations: int = 99, decSchedule: str = "F", OSDorder: int = -1,
-             rngSeed: Optional[int] = None, *, batch_size: int = 1 << 16, verbose: bool = True,
+             rngSeed: Optional[int] = None, *, batch_size: Optional[int] = None, verbose: bool = True,
              return_results: bool = False, sampler: Optional[str] = None):
     """p-sweep + results table (simulator.py:319-347). Returns None like the
     reference unless return_results=True."""
@@ -342,7 +362,8 @@ def main(argv=None):
     parser.add_argument("--decSchedule", choices=["F", "L", "S"], default="F",
                         help="Decoder scheduling method: [F] flooding; [L] layered; [S] serial.")
     parser.add_argument("--OSDorder", type=int, default=-1, help="Ordered Statistics Decoding order.")
-    parser.add_argument("--batch", type=int, default=1 << 16, help="Shots per GPU batch.")
+    parser.add_argument("--batch", type=int, default=None,
+                        help="Shots per batch (default 2^18 on the GPU, 2^16 on the host path).")
     parser.add_argument("--sampler", choices=["device", "host"], default=None,
                         help="Where shots are sampled and counted (default: device if present).")
     args = parser.parse_args(argv)

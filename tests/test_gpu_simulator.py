@@ -68,13 +68,14 @@ def test_device_channel_counters_equal_host_counters():
     Hx, Hz = codes.load_code("LP118_0")
     ch = simulator.DeviceChannel(Hx, Hz, torch.device("cuda", 0), 123)
     p = 0.06
-    sy_z, sy_x, errX, errZ = ch.sample(p, 50000)
+    sy_z, sy_x, errXw, errZw = ch.sample(p, 50000)
+    errX, errZ = ch.unpack(errXw), ch.unpack(errZw)
     ex = errX.cpu().numpy()
     assert abs(ex.mean() - 2 * p / 3) < 0.002
     np.testing.assert_array_equal(sy_z.cpu().numpy(), (ex.astype(np.int64) @ Hz.T) % 2)
     rX = decoders.decode_batch(Hz, sy_z, p / 3, 30)
     rZ = decoders.decode_batch(Hx, sy_x, p / 3, 30)
-    dev = ch.count(sy_z, sy_x, errX, errZ, rX.ehat, rZ.ehat, rX.iters, rZ.iters)
+    dev = ch.count(sy_z, sy_x, errXw, errZw, rX.ehat, rZ.ehat, rX.iters, rZ.iters)
     host = simulator.count_outcomes(Hx, Hz, sy_z.cpu().numpy(), sy_x.cpu().numpy(), ex,
                                     errZ.cpu().numpy(), rX.ehat.cpu().numpy(), rZ.ehat.cpu().numpy(),
                                     rX.iters.cpu().numpy(), rZ.iters.cpu().numpy())
@@ -96,3 +97,105 @@ def test_device_sampler_simulate_p_with_osd_agrees_with_host_sampler():
     for k in ("decSuccessExact",):
         assert abs(d[k] - h[k]) < 5 * np.sqrt(kw["shots"] * 0.25)
     assert abs(d["Avg_number_of_iterations_X"] - h["Avg_number_of_iterations_X"]) < 0.2
+
+
+@pytest.mark.parametrize("code,p,shot0,B", [
+    ("LP118_0", 0.06, 0, 3000),
+    ("LP04_0", 0.2, (1 << 32) - 700, 1500),    # the shot counter's high word carries
+    ("LP118_2", 0.01, 12345, 1000),
+    ("steane", 0.5, 7, 4000),
+    ("LP04_0", 1.0, 0, 64),                    # T3 = 2^32: every qubit errs
+    ("LP04_0", 0.0, 0, 64),
+])
+def test_device_sampler_bit_exact_vs_oracle_stream(code, p, shot0, B):
+    """qldpc_channel_sample reproduces the oracle's Philox stream bit for bit
+    (errors and syndromes), and batching does not change the stream."""
+    import torch
+    from oracle import oracle
+    from qldpcsim_amd import codes, simulator
+    Hx, Hz = codes.load_code(code)
+    seed = 0x9E3779B97F4A7C15
+    ch = simulator.DeviceChannel(Hx, Hz, torch.device("cuda", 0), seed, shot0=shot0)
+    a = ch.sample(p, B // 3)
+    b = ch.sample(p, B - B // 3)
+    got = [torch.cat([x, y]).cpu().numpy() for x, y in zip(a, b)]
+    got[2] = ch.unpack(torch.cat([a[2], b[2]])).cpu().numpy()
+    got[3] = ch.unpack(torch.cat([a[3], b[3]])).cpu().numpy()
+    want = oracle.channel_sample(Hx, Hz, p, seed, shot0, B)
+    for g, w, name in zip(got, want, ("sy_z", "sy_x", "errX", "errZ")):
+        np.testing.assert_array_equal(g, w, err_msg=name)
+    # padding bits of the last word stay zero
+    n = Hx.shape[1]
+    if n % 64:
+        assert int((a[2][:, -1] >> (n % 64)).abs().sum()) == 0
+
+
+@pytest.mark.parametrize("code,p", [("LP118_0", 0.08), ("LP04_0", 0.15), ("steane", 0.2)])
+def test_device_counters_match_reference_loop_with_crafted_estimates(code, p):
+    """Counters on estimates built to hit every branch (exact, degenerate-
+    style differences on zero-weight columns, failures, iteration sums) equal
+    the reference's per-shot loop (simulator.py:291-303)."""
+    import torch
+    from qldpcsim_amd import codes, simulator
+    Hx, Hz = codes.load_code(code)
+    dev = torch.device("cuda", 0)
+    ch = simulator.DeviceChannel(Hx, Hz, dev, 5)
+    B = 2000
+    sy_z, sy_x, ewX, ewZ = ch.sample(p, B)
+    errX = ch.unpack(ewX).cpu().numpy()
+    errZ = ch.unpack(ewZ).cpu().numpy()
+    rng = np.random.default_rng(1)
+    eX = errX.copy()
+    eZ = errZ.copy()
+    flip = rng.random((B, eX.shape[1])) < 0.002
+    eX ^= flip.astype(np.uint8) * (rng.random(B) < 0.5)[:, None].astype(np.uint8)
+    eZ ^= (rng.random((B, eZ.shape[1])) < 0.001).astype(np.uint8)
+    itX = rng.integers(1, 60, B).astype(np.int32)
+    itZ = rng.integers(1, 60, B).astype(np.int32)
+    T = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=dev)  # noqa: E731
+    got = ch.count(sy_z, sy_x, ewX, ewZ, T(eX), T(eZ), T(itX), T(itZ))
+    syz, syx = sy_z.cpu().numpy(), sy_x.cpu().numpy()
+    want = dict.fromkeys(simulator.COUNTER_KEYS, 0)
+    for k in range(B):
+        if np.array_equal(errX[k], eX[k]) and np.array_equal(errZ[k], eZ[k]):
+            want["decSuccessExact"] += 1
+        elif ((Hz.astype(int) @ (errX[k].astype(int) ^ eX[k])) == 0).all() and \
+                ((Hx.astype(int) @ (errZ[k].astype(int) ^ eZ[k])) == 0).all():
+            want["decSuccessDegen"] += 1
+        want["DecFailures_X"] += int(not np.array_equal(syz[k], (Hz.astype(int) @ eX[k]) % 2))
+        want["DecFailures_Z"] += int(not np.array_equal(syx[k], (Hx.astype(int) @ eZ[k]) % 2))
+    want["nIterAccX"] = int(itX.sum())
+    want["nIterAccZ"] = int(itZ.sum())
+    assert got == want
+    assert 0 < want["decSuccessExact"] < B and want["DecFailures_X"] > 0
+
+
+def test_device_counters_degenerate_branch_on_zero_weight_columns():
+    """A matrix with an all-zero column: a difference supported there is
+    'degenerate' under the reference's integer test (simulator.py:296)."""
+    import torch
+    from qldpcsim_amd import simulator
+    rng = np.random.default_rng(3)
+    n = 70
+    Hx = (rng.random((12, n)) < 0.2).astype(np.uint8)
+    Hz = (rng.random((10, n)) < 0.2).astype(np.uint8)
+    Hx[:, 65] = 0
+    Hz[:, 65] = 0
+    Hz[:, 3] = 0
+    dev = torch.device("cuda", 0)
+    ch = simulator.DeviceChannel(Hx, Hz, dev, 9)
+    B = 300
+    sy_z, sy_x, ewX, ewZ = ch.sample(0.1, B)
+    errX = ch.unpack(ewX).cpu().numpy()
+    errZ = ch.unpack(ewZ).cpu().numpy()
+    eX, eZ = errX.copy(), errZ.copy()
+    eX[::3, 65] ^= 1
+    eX[1::5, 3] ^= 1
+    eZ[::7, 65] ^= 1
+    eZ[2::11, 3] ^= 1                     # column 3 of Hx is nonzero: not degenerate
+    it = np.ones(B, np.int32)
+    T = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=dev)  # noqa: E731
+    got = ch.count(sy_z, sy_x, ewX, ewZ, T(eX), T(eZ), T(it), T(it))
+    want = simulator.count_outcomes(Hx, Hz, sy_z.cpu().numpy(), sy_x.cpu().numpy(), errX, errZ,
+                                    eX, eZ, it, it)
+    assert got == want and want["decSuccessDegen"] > 0

@@ -117,3 +117,47 @@ def test_results_table_format():
     txt = format_results([0.01], [r], 1000)
     assert "SIMULATION RESULTS" in txt
     assert "  1.00e-02  " in txt and "1.00e-02" in txt and "    3,    4" in txt and " 1.25,  1.50" in txt
+
+
+def test_oracle_philox_known_answer_vectors():
+    """The oracle's Philox4x32-10 block function reproduces the published
+    known-answer vectors (Random123 kat_vectors, philox4x32_10)."""
+    import ctypes
+    from oracle import oracle
+    L = oracle.lib()
+    kat = [((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+           ((0xffffffff,) * 4, (0xffffffff,) * 2, (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+           ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0),
+            (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1))]
+    for ctr, key, want in kat:
+        c = np.array(ctr, np.uint32)
+        L.oracle_philox4x32_10(c.ctypes.data_as(ctypes.c_void_p), ctypes.c_uint32(key[0]),
+                               ctypes.c_uint32(key[1]))
+        assert tuple(int(x) for x in c) == want
+
+
+def test_oracle_channel_stream_statistics_and_thresholds():
+    """The sampler stream restatement: X/Y/Z each p/3 per qubit (simulator.py:107),
+    syndromes H·e mod 2, thresholds match the C ABI's."""
+    import ctypes
+    from oracle import oracle
+    from qldpcsim_amd import _lib, codes
+    for p in (0.0, 0.01, 0.3, 1.0):
+        t = [ctypes.c_uint64() for _ in range(3)]
+        _lib.check(_lib.lib.qldpc_channel_thresholds(p, *(ctypes.byref(x) for x in t)))
+        assert tuple(x.value for x in t) == oracle.channel_thresholds(p)
+    with pytest.raises(ValueError):
+        _lib.check(_lib.lib.qldpc_channel_thresholds(1.5, None, None, None))
+    Hx, Hz = codes.load_code("LP04_0")
+    p = 0.09
+    sz, sx, ex, ez = oracle.channel_sample(Hx, Hz, p, 77, 0, 6000)
+    N = ex.size
+    y = (ex & ez).mean()
+    assert abs(y - p / 3) < 5 * np.sqrt(p / 3 / N)
+    assert abs((ex & (1 - ez)).mean() - p / 3) < 5 * np.sqrt(p / 3 / N)
+    assert abs((ez & (1 - ex)).mean() - p / 3) < 5 * np.sqrt(p / 3 / N)
+    np.testing.assert_array_equal(sz, (ex.astype(np.int64) @ Hz.T) % 2)
+    np.testing.assert_array_equal(sx, (ez.astype(np.int64) @ Hx.T) % 2)
+    # the stream is a function of (seed, shot): an offset window matches
+    w = oracle.channel_sample(Hx, Hz, p, 77, 1000, 50)
+    np.testing.assert_array_equal(w[2], ex[1000:1050])

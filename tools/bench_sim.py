@@ -13,7 +13,7 @@ from qldpcsim_amd import codes, simulator  # noqa: E402
 
 
 def main():
-    shots = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 18
+    shots = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
     runs = [
         ("LP118_2", "MS", "L", 0, 50),      # configs[3]: MS layered + OSD-0
         ("LP118_2", "BP", "L", 4, 100),     # configs[4]: BP layered (+OSD 4: ignored by simulate)
@@ -26,7 +26,7 @@ def main():
                                  decSchedule=sched, OSDorder=osd, rngSeed=1, verbose=False)  # warm-up
             t0 = time.perf_counter()
             r = simulator.simulate_p(Hx, Hz, p, shots=shots, decType=dec, decIterations=it,
-                                     decSchedule=sched, OSDorder=osd, rngSeed=1, batch_size=1 << 16,
+                                     decSchedule=sched, OSDorder=osd, rngSeed=1,
                                      verbose=False)
             dt = time.perf_counter() - t0
             qbler = 1. - (r["decSuccessExact"] + r["decSuccessDegen"]) / shots
