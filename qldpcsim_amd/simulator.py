@@ -328,22 +328,61 @@ def format_results(p, results, shots):
     return "\n".join(lines)
 
 
+def _load_results(path, meta):
+    """Per-p results already in a resumable results file (JSON), if its
+    run parameters match `meta`; else empty."""
+    import json
+    import os
+    if not path or not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        doc = json.load(f)
+    if doc.get("meta") != meta:
+        raise ValueError(f"{path} holds results of a different run: {doc.get('meta')}")
+    return {float(k): v for k, v in doc.get("results", {}).items()}
+
+
+def _save_results(path, meta, done):
+    import json
+    import os
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump({"meta": meta, "results": {repr(k): v for k, v in sorted(done.items())}}, f, indent=1)
+    os.replace(tmp, path)                      # atomic: a killed run leaves the last good file
+
+
 def simulate(HxFile: str, HzFile: str, p, shots: int = 1000, decType: str = "MS",
              decIterations: int = 99, decSchedule: str = "F", OSDorder: int = -1,
              rngSeed: Optional[int] = None, *, batch_size: Optional[int] = None, verbose: bool = True,
-             return_results: bool = False, sampler: Optional[str] = None):
+             return_results: bool = False, sampler: Optional[str] = None,
+             resultsFile: Optional[str] = None):
     """p-sweep + results table (simulator.py:319-347). Returns None like the
-    reference unless return_results=True."""
+    reference unless return_results=True.
+
+    resultsFile (extension): a JSON file the sweep writes after every
+    p-point; a rerun with the same arguments skips the points already there
+    (resumable long sweeps). Only rank 0 writes it."""
     Hx = load_matrix(HxFile)
     Hz = load_matrix(HzFile)
     assert max(p) <= 1. and min(p) >= 0.
+    _, rank, world = _dist()
+    meta = {"Hx": HxFile, "Hz": HzFile, "shots": shots, "decType": decType,
+            "decIterations": decIterations, "decSchedule": decSchedule, "OSDorder": OSDorder,
+            "rngSeed": rngSeed, "world": world}
+    done = _load_results(resultsFile, meta)
     results = []
     for pT in p:
-        results.append(simulate_p(Hx, Hz, p=pT, shots=shots, rngSeed=rngSeed, decType=decType,
-                                  decIterations=decIterations, decSchedule=decSchedule,
-                                  OSDorder=OSDorder, batch_size=batch_size, verbose=verbose,
-                                  sampler=sampler))
-    _, rank, _ = _dist()
+        if float(pT) in done:
+            results.append(done[float(pT)])
+            continue
+        r = simulate_p(Hx, Hz, p=pT, shots=shots, rngSeed=rngSeed, decType=decType,
+                       decIterations=decIterations, decSchedule=decSchedule,
+                       OSDorder=OSDorder, batch_size=batch_size, verbose=verbose,
+                       sampler=sampler)
+        results.append(r)
+        done[float(pT)] = r
+        if resultsFile and rank == 0:
+            _save_results(resultsFile, meta, done)
     if rank == 0:
         print(format_results(p, results, shots))
     return results if return_results else None
@@ -366,6 +405,8 @@ def main(argv=None):
                         help="Shots per batch (default 2^18 on the GPU, 2^16 on the host path).")
     parser.add_argument("--sampler", choices=["device", "host"], default=None,
                         help="Where shots are sampled and counted (default: device if present).")
+    parser.add_argument("--results", default=None,
+                        help="Resumable results file (JSON, written after every p-point).")
     args = parser.parse_args(argv)
     print("\n   Command line arguments:")
     print(args)
@@ -373,7 +414,7 @@ def main(argv=None):
     simulate(HxFile=args.Hx, HzFile=args.Hz, p=args.p, shots=args.shots, decType=args.decType,
              decIterations=args.decIterations, decSchedule=args.decSchedule,
              OSDorder=args.OSDorder, rngSeed=args.rngSeed, batch_size=args.batch,
-             sampler=args.sampler)
+             sampler=args.sampler, resultsFile=args.results)
 
 
 if __name__ == "__main__":

@@ -161,3 +161,29 @@ def test_oracle_channel_stream_statistics_and_thresholds():
     # the stream is a function of (seed, shot): an offset window matches
     w = oracle.channel_sample(Hx, Hz, p, 77, 1000, 50)
     np.testing.assert_array_equal(w[2], ex[1000:1050])
+
+
+def test_resumable_results_file(tmp_path, monkeypatch):
+    """simulate(resultsFile=...) writes each p-point as it finishes and a rerun
+    skips the points already there; a file from another run is refused."""
+    from qldpcsim_amd import simulator
+    calls = []
+
+    def fake_simulate_p(Hx, Hz, p, **kw):
+        calls.append(p)
+        return {"DecFailures_X": 1, "DecFailures_Z": 2, "decSuccessExact": 90, "decSuccessDegen": 0,
+                "Avg_number_of_iterations_X": 1.5, "Avg_number_of_iterations_Z": p}
+
+    monkeypatch.setattr(simulator, "simulate_p", fake_simulate_p)
+    Hx, Hz = codes.load_code("steane")
+    np.save(tmp_path / "Hx.npy", Hx)
+    np.save(tmp_path / "Hz.npy", Hz)
+    f = str(tmp_path / "res.json")
+    kw = dict(shots=100, rngSeed=1, verbose=False, return_results=True, resultsFile=f)
+    a = simulator.simulate(str(tmp_path / "Hx.npy"), str(tmp_path / "Hz.npy"), [0.01, 0.02], **kw)
+    assert calls == [0.01, 0.02]
+    b = simulator.simulate(str(tmp_path / "Hx.npy"), str(tmp_path / "Hz.npy"), [0.01, 0.02, 0.05], **kw)
+    assert calls == [0.01, 0.02, 0.05] and b[:2] == a
+    with pytest.raises(ValueError):
+        simulator.simulate(str(tmp_path / "Hx.npy"), str(tmp_path / "Hz.npy"), [0.01],
+                           **{**kw, "shots": 200})
