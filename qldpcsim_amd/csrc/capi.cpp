@@ -1033,7 +1033,7 @@ extern "C" int qldpc_osd_device(const qldpc_code* code, int64_t count, const uin
   const void* k = qldpc::select_osd_kernel(nw);
   if (!k) return fail(QLDPC_EUNSUP, "GPU OSD supports n <= 2111 columns (got %d)", n);
   int lds = 4 * n + 4 * (m + 2) + n;
-  lds = align16(lds) + 8 * 3 * nw + 4 * 32 + 16;
+  lds = align16(lds) + 8 * nw * (1 + 2 * 16 + 2) + 4 * 32 + 16;  // emask, candidate / xrow rows, slots
   if (order == 1) lds += 4 * setdiff_table_ints(n);
   int dev = 0, max_lds = 0;
   HIP_TRY(hipGetDevice(&dev));

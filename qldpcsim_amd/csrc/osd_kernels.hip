@@ -32,17 +32,20 @@ __device__ int first_setdiff(int n, const unsigned char* inJ, int nJ, int* table
 
 template <int NW>
 __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
-  // LDS: inv_perm[n] | J list [m+1] | inJ bytes [n] | emask [NW] u64 |
-  //      pivot row [NW] | swap row [NW] | wave slots [2][16] | set table
+  // LDS: inv_perm[n] | J list [m+2] | inJ bytes [n] | emask [NW] u64 |
+  //      candidate rows [2][16][NW] | xrow rows [2][NW] | candidate ids [2][16] |
+  //      misc [4] | set table
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int m = a.m, n = a.n;
   int* inv = (int*)lds;
   int* Jl = inv + n;
   unsigned char* inJ = (unsigned char*)(Jl + m + 2);
-  uint64_t* emask = (uint64_t*)(((uintptr_t)(inJ + n) + 15) & ~(uintptr_t)15);
-  uint64_t* pivbuf = emask + NW;
-  uint64_t* swapbuf = pivbuf + NW;
-  int* slots = (int*)(swapbuf + NW);               // [2][16]
+  // offsets from `lds` itself (a cast through an integer would turn every
+  // access below into a generic flat access instead of ds_read / ds_write)
+  uint64_t* emask = (uint64_t*)(lds + ((4 * (n + m + 2) + n + 15) & ~15));
+  uint64_t* cbuf = emask + NW;                     // [2][16][NW]
+  uint64_t* xbuf = cbuf + 2 * 16 * NW;             // [2][NW]
+  int* slots = (int*)(xbuf + 2 * NW);              // [2][16]
   int* misc = slots + 32;                          // [0]=|J| [1]=status [2]=first info index
   int* table = misc + 4;                           // CPython set emulation (order 1)
 
@@ -59,7 +62,8 @@ __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
   }
   __syncthreads();
 
-  // my row of Hp (+ syndrome bit at column n)
+  // my row of Hp (+ syndrome bit at column n); thread t holds the row at
+  // position t of REF's current row order (rows move by REF's swaps)
   uint64_t R[NW];
 #pragma unroll
   for (int w = 0; w < NW; ++w) R[w] = 0;
@@ -85,6 +89,15 @@ __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
     inJ[0] = 1;
   }
   nJ = 1;
+  // One workgroup barrier per column. Before it, each wave's first candidate
+  // row (a 1 in column i at a position >= xrow) and the row at position xrow
+  // publish their words >= w; after it, every thread knows the pivot (the
+  // smallest candidate position: REF's "first row at or below") and reads its
+  // row from the winning wave's slot. Rows at positions >= xrow are zero in
+  // every column < i (a nonzero there would have been a pivot), so words < w
+  // never need to move. Two slot sets alternate: a wave writing set s at
+  // column k+2 has passed column k+1's barrier, which every reader of column
+  // k's set s had reached after its reads.
   // Fully unrolled over the NW words, so every R[w] / R[q] index is a
   // compile-time constant and the row stays in VGPRs (a runtime word index
   // would put R in scratch memory: one global access per touch).
@@ -96,8 +109,23 @@ __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
       if (i >= n || done) break;
       const bool has = own && ((R[w] >> b) & 1ull);
       const uint64_t bal = __ballot(has && t >= xrow);
-      int* sl = slots + 16 * (step & 1);
-      if (lane == 0) sl[wave] = bal ? wave * 64 + __builtin_ctzll(bal) : 0x7fffffff;
+      const int set = step & 1;
+      uint64_t* cb = cbuf + (set * 16 + wave) * NW;
+      uint64_t* xb = xbuf + set * NW;
+      int* sl = slots + 16 * set;
+      if (bal) {
+        if (lane == __builtin_ctzll(bal)) {
+#pragma unroll
+          for (int q = w; q < NW; ++q) cb[q] = R[q];
+          sl[wave] = t;
+        }
+      } else if (lane == 0) {
+        sl[wave] = 0x7fffffff;
+      }
+      if (t == xrow) {
+#pragma unroll
+        for (int q = w; q < NW; ++q) xb[q] = R[q];
+      }
       __syncthreads();
       int piv = 0x7fffffff;
       for (int q = 0; q < nwaves; ++q) piv = min(piv, sl[q]);
@@ -105,24 +133,16 @@ __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
       if (piv == 0x7fffffff) continue;              // dependent column: not in J
       // pivot row `piv` moves to position xrow (REF's row swap), then every
       // other row holding a 1 in column i is XOR-ed with it (below and above)
-      if (t == piv) {
-#pragma unroll
-        for (int q = w; q < NW; ++q) pivbuf[q] = R[q];  // the pivot row is 0 left of word w
-      }
-      if (t == xrow && piv != xrow) {
-#pragma unroll
-        for (int q = 0; q < NW; ++q) swapbuf[q] = R[q];
-      }
-      __syncthreads();
+      const uint64_t* pr = cbuf + (set * 16 + (piv >> 6)) * NW;
       if (t == piv && piv != xrow) {
 #pragma unroll
-        for (int q = 0; q < NW; ++q) R[q] = swapbuf[q];   // old row xrow: 0 in column i
+        for (int q = w; q < NW; ++q) R[q] = xb[q];   // old row xrow: 0 in column i
       } else if (t == xrow) {
 #pragma unroll
-        for (int q = 0; q < NW; ++q) R[q] = q < w ? 0ull : pivbuf[q];
+        for (int q = w; q < NW; ++q) R[q] = pr[q];
       } else if (has) {
 #pragma unroll
-        for (int q = w; q < NW; ++q) R[q] ^= pivbuf[q];  // pivot row is 0 left of column i
+        for (int q = w; q < NW; ++q) R[q] ^= pr[q];  // pivot row is 0 left of column i
       }
       if (i != 0) {
         if (t == 0) {
@@ -142,14 +162,13 @@ __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
     return;
   }
   __syncthreads();
-  // information-set values e_I (e_perm = e_hat[perm], decoders.py:345)
-  for (int w = t; w < NW; w += blockDim.x) {
-    uint64_t bits = 0;
-    for (int b = 0; b < 64; ++b) {
-      const int i = 64 * w + b;
-      if (i < n && !inJ[i] && (ehat[perm[i]] & 1)) bits |= 1ull << b;
-    }
-    emask[w] = bits;
+  // information-set values e_I (e_perm = e_hat[perm], decoders.py:345):
+  // one column per thread, words assembled by ballots (all loads in flight)
+  for (int i0w = 64 * wave; i0w < 64 * NW; i0w += blockDim.x) {
+    const int i = i0w + lane;
+    const bool bit = i < n && !inJ[i] && (ehat[perm[i]] & 1);
+    const uint64_t bits = __ballot(bit);
+    if (lane == 0) emask[i0w >> 6] = bits;
   }
   if (t == 0) {
     int i0 = -1;
