@@ -14,4 +14,4 @@ timeout -k 10 -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpur
 timeout -k 10 -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write_$TAG -o pmc -- python3 bench.py --steps 1 --warmup 0 --cpu-seconds 0 > gpurun_out/bench_pmc_write.log 2>&1 || exit $?
 bash tools/gpu_counters.sh $TAG || exit $?
 timeout -k 10 900 python tools/bench_configs.py > gpurun_out/configs_$TAG.jsonl 2> gpurun_out/configs_$TAG.err || exit $?
-timeout -k 10 900 python tools/bench_sim.py 262144 > gpurun_out/sim_$TAG.jsonl 2> gpurun_out/sim_$TAG.err || exit $?
+timeout -k 10 900 python tools/bench_sim.py > gpurun_out/sim_$TAG.jsonl 2> gpurun_out/sim_$TAG.err || exit $?
