@@ -15,10 +15,12 @@
  *
  * Method: tanh = e/(e+2), e = expm1(2|x|) (Cody–Waite reduction y = k ln2 + r,
  * |r| <= ln2/2, degree-14 Taylor polynomial, 2^k (1 + expm1 r) - 1
- * reassembled exactly); atanh = log1p(2|x|/(1-|x|))/2 with log1p as fdlibm
- * (f itself inside (1/sqrt2-1, sqrt2-1), else u = 1+f = 2^k m with rounding
- * correction c; log(1+f') = f' - hfsq + s (hfsq + R(s^2)), s = f'/(2+f')).
- * Written branch-light (one division each) because GPU lanes diverge.
+ * reassembled exactly); atanh(a) = k ln2/2 + atanh(s), s = (N - D 2^k) /
+ * (N + D 2^k) with N = 1 + a and D = 1 - a held as exact two-term sums and
+ * 2^k the power of two nearest N / D (|s| <= 3 - 2 sqrt2; odd series in s).
+ * One division each and no data-dependent branches below the special values,
+ * because GPU lanes diverge (atanh: 133 -> ~60 gfx950 instructions; fewer
+ * 2-3 ULP cases than the fdlibm log1p form it replaced).
  */
 #ifndef QLDPC_LIBM_H
 #define QLDPC_LIBM_H
@@ -74,24 +76,20 @@ QLDPC_HD double qldpc_expm1_pos(double y) {
   const double fk = (double)k;
   const double r = QLDPC_FMA(-fk, QLDPC_LN2_LO, y - fk * QLDPC_LN2_HI);  /* fk*LN2_HI exact */
   const double em = qldpc_expm1_small(r);
-  if (k == 0) return em;
   const double two_k = qldpc_bits2d((uint64_t)(k + 1023) << 52);
-  return QLDPC_FMA(two_k, em, two_k - 1.0);      /* two_k - 1 exact for k <= 53 */
+  return QLDPC_FMA(two_k, em, two_k - 1.0);      /* two_k - 1 exact for k <= 53; k = 0: em */
 }
 
 QLDPC_HD double qldpc_tanh(double x) {
   const uint64_t sgn = qldpc_d2bits(x) & 0x8000000000000000ull;
   const double a = qldpc_bits2d(qldpc_d2bits(x) & 0x7fffffffffffffffull);
-  double t;
   if (!(a == a)) return x;                        /* NaN */
-  if (a >= 22.0) {
-    t = 1.0;                                      /* 1 - tanh(22) < 2^-62 */
-  } else if (a < 3.7252902984e-09) {              /* 2^-28: tanh(x) = x in double */
-    t = a;
-  } else {
-    const double em = qldpc_expm1_pos(a + a);
-    t = em / (em + 2.0);                          /* one division, any a (<= 3 ULP) */
-  }
+  /* branch-free (lanes diverge): the range cases are selects */
+  const double ac = a < 22.0 ? a : 22.0;
+  const double em = qldpc_expm1_pos(ac + ac);
+  double t = em / (em + 2.0);                     /* one division, any a (<= 3 ULP) */
+  t = a >= 22.0 ? 1.0 : t;                        /* 1 - tanh(22) < 2^-62 */
+  t = a < 3.7252902984e-09 ? a : t;               /* 2^-28: tanh(x) = x in double */
   return qldpc_bits2d(qldpc_d2bits(t) | sgn);
 }
 
@@ -151,18 +149,51 @@ QLDPC_HD double qldpc_log1p(double f) {
   return QLDPC_FMA(fk, QLDPC_LN2_HI, (fm - QLDPC_FMA(-s, hfsq + R, hfsq)) + QLDPC_FMA(fk, QLDPC_LN2_LO, c));
 }
 
+/* atanh(s) for |s| <= 0.1716: s + s^3 (1/3 + s^2/5 + ... + s^20/21)
+   (first omitted term < 2^-60 |s|) */
+QLDPC_HD double qldpc_atanh_small(double s) {
+  const double z = s * s;
+  double q = 1.0 / 21.0;
+  q = QLDPC_FMA(q, z, 1.0 / 19.0);
+  q = QLDPC_FMA(q, z, 1.0 / 17.0);
+  q = QLDPC_FMA(q, z, 1.0 / 15.0);
+  q = QLDPC_FMA(q, z, 1.0 / 13.0);
+  q = QLDPC_FMA(q, z, 1.0 / 11.0);
+  q = QLDPC_FMA(q, z, 1.0 / 9.0);
+  q = QLDPC_FMA(q, z, 1.0 / 7.0);
+  q = QLDPC_FMA(q, z, 1.0 / 5.0);
+  q = QLDPC_FMA(q, z, 1.0 / 3.0);
+  return QLDPC_FMA(s * z, q, s);
+}
+
+/* atanh(a) = atanh(s) + k ln2 / 2 with s = (N - D 2^k) / (N + D 2^k),
+   N = 1 + a, D = 1 - a (ratio of the two = 2^k m, m in [sqrt2/2, sqrt2],
+   so |s| <= 3 - 2 sqrt2). N and D are carried as exact two-term sums (their
+   rounding errors by Fast2Sum), N - D 2^k is exact (Sterbenz) and the
+   corrections enter once: one division in all, no logarithm. Below
+   3 - 2 sqrt2, k = 0 and s = a exactly. */
 QLDPC_HD double qldpc_atanh(double x) {
   const uint64_t sgn = qldpc_d2bits(x) & 0x8000000000000000ull;
   const double a = qldpc_bits2d(qldpc_d2bits(x) & 0x7fffffffffffffffull);
-  double t;
   if (!(a == a)) return x;
-  if (a >= 1.0) {
-    t = (a == 1.0) ? qldpc_bits2d(0x7ff0000000000000ull) : qldpc_bits2d(0x7ff8000000000000ull);
-  } else if (a < 3.7252902984e-09) {
-    t = a;                                        /* atanh(x) = x in double */
-  } else {
-    t = 0.5 * qldpc_log1p((a + a) / (1.0 - a));   /* one division, any a (<= 3 ULP) */
-  }
+  if (a >= 1.0)
+    return qldpc_bits2d(((a == 1.0) ? 0x7ff0000000000000ull : 0x7ff8000000000000ull) | sgn);
+  /* branch-free below 1 (lanes diverge): both ranges share one series */
+  const double N = 1.0 + a, eN = (1.0 - N) + a;    /* N + eN = 1 + a exactly */
+  const double D = 1.0 - a, eD = (1.0 - D) - a;    /* D + eD = 1 - a exactly */
+  /* k = round(log2(N / D)): N in [1, 2); D = 2^-e mD, mD in [1, 2) */
+  const uint64_t db = qldpc_d2bits(D);
+  int k = 1023 - (int)((db >> 52) & 0x7ff);         /* e */
+  const double mD = qldpc_bits2d((db & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
+  if (N > 1.4142135623730951 * mD) k += 1;          /* N / (D 2^k) into [sqrt2/2, sqrt2] */
+  const double p2k = qldpc_bits2d((uint64_t)(1023 + k) << 52);
+  const double Dk = D * p2k, eDk = eD * p2k;        /* exact */
+  const double num = (N - Dk) + (eN - eDk);         /* N - Dk exact (Sterbenz) */
+  const double den = (N + Dk) + (eN + eDk);
+  const int big = a > 0.17157287525381;             /* 3 - 2 sqrt2 (rounded down) */
+  const double sr = big ? num / den : a;            /* below: k = 0, s = a exactly */
+  const double fk = big ? (double)k : 0.0;
+  const double t = QLDPC_FMA(fk, 0.5 * QLDPC_LN2_HI, qldpc_atanh_small(sr) + fk * (0.5 * QLDPC_LN2_LO));
   return qldpc_bits2d(qldpc_d2bits(t) | sgn);
 }
 

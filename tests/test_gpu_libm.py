@@ -32,8 +32,9 @@ extern "C" int run(const double* hx, double* ht, double* ha, double* hl, long n)
 '''
 C_SRC = r'''
 #include "qldpc_libm.h"
-void run(const double* x, double* t, double* a, double* l, long n) {
+int run(const double* x, double* t, double* a, double* l, long n) {
   for (long i = 0; i < n; ++i) { t[i] = qldpc_tanh(x[i]); a[i] = qldpc_atanh(x[i]); l[i] = qldpc_log1p(x[i]); }
+  return 0;
 }
 '''
 
