@@ -14,7 +14,9 @@ launch per half (X: Hz with the Hx-derived layers; Z: Hx with the
 Hz-derived layers, the reference's cross-wiring, :278-282) — and the counters
 are formed with array operations with the reference's exact definitions.
 With torch.distributed initialised, shots shard across ranks and the six
-counters are summed with one all_reduce (RCCL over xGMI on the GPU node).
+counters are summed with one all_reduce (RCCL over xGMI on the GPU node);
+`torchrun --nproc-per-node 8 -m qldpcsim_amd.simulator ...` sets that up
+(one process per GPU).
 
 Syndrome source: Stim is not available in this environment,
 so shots come from a per-qubit Pauli sampler (X, Y, Z each p/3 — the
@@ -388,6 +390,30 @@ def simulate(HxFile: str, HzFile: str, p, shots: int = 1000, decType: str = "MS"
     return results if return_results else None
 
 
+def _init_dist_from_env():
+    """One process per GPU under torchrun (WORLD_SIZE > 1 in the environment):
+    bind this rank to its device and join the process group (RCCL over xGMI;
+    QLDPC_SIM_BACKEND=gloo to rehearse on CPU or with ranks sharing a GPU).
+    Returns True if this call created the group."""
+    import os
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        return False
+    import torch
+    import torch.distributed as dist
+    if dist.is_initialized():
+        return False
+    backend = os.environ.get("QLDPC_SIM_BACKEND", "nccl" if torch.cuda.is_available() else "gloo")
+    if torch.cuda.is_available():
+        local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            return True
+    dist.init_process_group(backend)
+    return True
+
+
 def main(argv=None):
     parser = argparse.ArgumentParser(description="Stim-based QC-LDPC depolarizing-channel simulator.")
     parser.add_argument("--Hx", required=True, help="Path to Hx parity-check matrix (.npy).")
@@ -408,13 +434,21 @@ def main(argv=None):
     parser.add_argument("--results", default=None,
                         help="Resumable results file (JSON, written after every p-point).")
     args = parser.parse_args(argv)
-    print("\n   Command line arguments:")
-    print(args)
-    print("")
-    simulate(HxFile=args.Hx, HzFile=args.Hz, p=args.p, shots=args.shots, decType=args.decType,
-             decIterations=args.decIterations, decSchedule=args.decSchedule,
-             OSDorder=args.OSDorder, rngSeed=args.rngSeed, batch_size=args.batch,
-             sampler=args.sampler, resultsFile=args.results)
+    own_group = _init_dist_from_env()              # torchrun: shots shard over the ranks
+    _, rank, _ = _dist()
+    if rank == 0:
+        print("\n   Command line arguments:")
+        print(args)
+        print("")
+    try:
+        simulate(HxFile=args.Hx, HzFile=args.Hz, p=args.p, shots=args.shots, decType=args.decType,
+                 decIterations=args.decIterations, decSchedule=args.decSchedule,
+                 OSDorder=args.OSDorder, rngSeed=args.rngSeed, batch_size=args.batch,
+                 sampler=args.sampler, resultsFile=args.results)
+    finally:
+        if own_group:
+            import torch.distributed as dist
+            dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -199,3 +199,36 @@ def test_device_counters_degenerate_branch_on_zero_weight_columns():
     want = simulator.count_outcomes(Hx, Hz, sy_z.cpu().numpy(), sy_x.cpu().numpy(), errX, errZ,
                                     eX, eZ, it, it)
     assert got == want and want["decSuccessDegen"] > 0
+
+
+def test_cli_two_ranks_shard_shots(tmp_path):
+    """`torchrun -m qldpcsim_amd.simulator` shards the shots over the ranks and
+    sums the counters (here 2 ranks share the one GPU over gloo; on the
+    8-GPU node one rank per GPU over RCCL)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    from qldpcsim_amd import codes, simulator
+    Hx, Hz = codes.load_code("LP04_0")
+    np.save(tmp_path / "Hx.npy", Hx.astype(np.int64))
+    np.save(tmp_path / "Hz.npy", Hz.astype(np.int64))
+    res = tmp_path / "res.json"
+    shots = 40001
+    env = dict(os.environ, QLDPC_SIM_BACKEND="gloo")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29533", "-m", "qldpcsim_amd.simulator",
+                        "--Hx", str(tmp_path / "Hx.npy"), "--Hz", str(tmp_path / "Hz.npy"), "--p", "0.08",
+                        "--shots", str(shots), "--decIterations", "30", "--rngSeed", "4",
+                        "--results", str(res)], cwd=ROOT, capture_output=True, text=True, timeout=110, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.count("SIMULATION RESULTS") == 1          # rank 0 prints the table
+    doc = json.loads(res.read_text())
+    assert doc["meta"]["world"] == 2
+    two = doc["results"]["0.08"]
+    one = simulator.simulate_p(Hx, Hz, 0.08, shots=shots, decIterations=30, rngSeed=4, verbose=False)
+    for k in ("decSuccessExact", "DecFailures_X"):
+        assert abs(two[k] - one[k]) < 6 * np.sqrt(shots * 0.25) + 5, (k, two[k], one[k])
+    assert two["decSuccessExact"] + two["decSuccessDegen"] <= shots
+    assert abs(two["Avg_number_of_iterations_X"] - one["Avg_number_of_iterations_X"]) < 0.1
