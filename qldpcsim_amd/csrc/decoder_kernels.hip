@@ -87,6 +87,73 @@ __device__ __forceinline__ void store_bits64(uint32_t* words, int c0, int pred, 
   if (lane == 1) words[(c0 >> 5) + 1] = (uint32_t)(b >> 32);
 }
 
+// Half-shot prologue / epilogue with every global load issued up front (a
+// loop of dependent load -> use steps paid one HBM latency per 64 elements).
+// The relabeling vinv is per code, so it is read once per kernel into
+// registers: VinvRegs holds original column 64k + lane's variable for k < NJ
+// (two 16-bit entries per VGPR); n > 64 NJ falls back to global reads.
+template <int NJ>
+struct VinvRegs {
+  uint32_t w[(NJ + 1) / 2];
+  __device__ __forceinline__ void load(const uint16_t* vinv, int n, int lane) {
+#pragma unroll
+    for (int k = 0; k < NJ; k += 2) {
+      const int j0 = 64 * k + lane, j1 = j0 + 64;
+      const uint32_t v0 = j0 < n ? vinv[j0] : 0u, v1 = j1 < n ? vinv[j1] : 0u;
+      w[k / 2] = v0 | (v1 << 16);
+    }
+  }
+  __device__ __forceinline__ int get(int k) const { return (int)((w[k / 2] >> (16 * (k & 1))) & 0xffffu); }
+};
+
+// ê (and posteriors) of one half-shot in original column order
+template <int NJ>
+__device__ __forceinline__ void write_outputs(const DecodeArgs& a, const VinvRegs<NJ>& vr, const double* post,
+                                              long long hs, int lane) {
+  const int n = a.n;
+  uint8_t* eh = a.ehat + hs * (long long)n;
+  double* po = a.post ? a.post + hs * (long long)n : nullptr;
+  if (n <= 64 * NJ) {
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) {
+      const int jo = 64 * k + lane;
+      if (64 * k < n && jo < n) {
+        const double pv = post[vr.get(k)];
+        eh[jo] = (uint8_t)(pv < 0.0);
+        if (po) po[jo] = pv;
+      }
+    }
+  } else {
+    for (int jo = lane; jo < n; jo += 64) {
+      const double pv = post[a.vinv[jo]];
+      eh[jo] = (uint8_t)(pv < 0.0);
+      if (po) po[jo] = pv;
+    }
+  }
+}
+
+// syndrome bits of one half-shot into the per-wave word array (m <= 64 NC:
+// all byte loads in flight together; larger m loops)
+template <int NC>
+__device__ __forceinline__ void load_syndrome_bits(const uint8_t* syn, int m, uint32_t* synw, int lane) {
+  if (m <= 64 * NC) {
+    uint32_t b[NC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const int c = 64 * k + lane;
+      b[k] = (64 * k < m && c < m) ? (uint32_t)(syn[c] & 1) : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < NC; ++k)
+      if (64 * k < m) store_bits64(synw, 64 * k, (int)b[k], lane);
+  } else {
+    for (int c0 = 0; c0 < m; c0 += 64) {
+      const int c = c0 + lane;
+      store_bits64(synw, c0, c < m ? (syn[c] & 1) : 0, lane);
+    }
+  }
+}
+
 // Persistent half-shot loop. Each wave starts with one static half-shot;
 // with a queue, further work comes from a global ticket counter in guided
 // chunks (about remaining / (4 * waves) consecutive half-shots, at most 64,
@@ -95,12 +162,21 @@ __device__ __forceinline__ void store_bits64(uint32_t* words, int c0, int pred, 
 // syndromes: most stop after 1-3 iterations, a few run max_iter) then
 // balance across waves instead of leaving a long tail, and the counter sees
 // O(waves * log) atomics rather than one per half-shot.
+// A wave-uniform 64-bit value the compiler may not prove uniform: pinning it
+// to scalar registers keeps the queue state out of VGPRs (the headline kernel
+// had spilled it to scratch memory at its 168-VGPR budget).
+__device__ __forceinline__ long long uniform64(long long x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+  return (long long)(((uint64_t)hi << 32) | lo);
+}
+
 struct HalfShotQueue {
   long long hs, end, stride, batch;
   uint32_t* q;
   uint32_t tk, tlen, seen;
   __device__ __forceinline__ HalfShotQueue(const DecodeArgs& a, int waves, int wid)
-      : hs((long long)blockIdx.x * waves + wid), end(0), stride((long long)gridDim.x * waves),
+      : hs(uniform64((long long)blockIdx.x * waves + wid)), end(0), stride((long long)gridDim.x * waves),
         batch(a.batch), q(a.queue), tk(0), tlen(1), seen(0) {
     end = hs + 1;
   }
@@ -115,14 +191,15 @@ struct HalfShotQueue {
   }
   __device__ __forceinline__ void advance() {
     if (!q) {
-      hs += stride;
+      hs = uniform64(hs + stride);
       return;
     }
-    if (++hs < end) return;
+    hs = uniform64(hs + 1);
+    if (hs < end) return;
     const uint32_t t = __builtin_amdgcn_readfirstlane(tk);
     seen = t + tlen;
-    hs = stride + (long long)t;
-    end = hs + tlen;
+    hs = uniform64(stride + (long long)t);
+    end = uniform64(hs + tlen);
   }
 };
 
@@ -997,6 +1074,8 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
   uint32_t* parw = (uint32_t*)(ws + a.off_parw);
   const int m = a.m, n = a.n;
   const int nwords = (m + 31) >> 5;
+  VinvRegs<16> vr;                                             // n <= 1024 in registers
+  vr.load(a.vinv, n, lane);
 
   for (HalfShotQueue Q(a, waves, wid); Q.hs < a.batch; Q.advance()) {
     const long long hs = Q.hs;
@@ -1006,14 +1085,11 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
     int iters = a.max_iter;
     bool conv = false;
     const double L = a.L;
+    load_syndrome_bits<8>(syn, m, synw, lane);
     for (int j = lane; j < n; j += 64) post[j] = L;             // v2c = L, c2v = 0 (:148-150)
     for (int p = lane; p < a.E; p += 64) c2v[p] = 0.0f;
-    for (int c0 = 0; c0 < m; c0 += 64) {
-      const int c = c0 + lane;
-      const int in = c < m;
-      store_bits64(synw, c0, in ? (syn[c] & 1) : 0, lane);
-      store_bits64(parw, c0, in && (L < 0.0) && (DC & 1), lane);
-    }
+    for (int c0 = 0; c0 < m; c0 += 64)
+      store_bits64(parw, c0, (c0 + lane < m) && (L < 0.0) && (DC & 1), lane);
     wave_sync();
     bool first = true;
     for (int it = 0; it < a.max_iter && !conv; ++it) {
@@ -1060,13 +1136,7 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
         }
       }
     }
-    uint8_t* eh = a.ehat + hs * (long long)n;
-    double* po = a.post ? a.post + hs * (long long)n : nullptr;
-    for (int jo = lane; jo < n; jo += 64) {
-      const double pv = post[a.vinv[jo]];
-      eh[jo] = (uint8_t)(pv < 0.0);
-      if (po) po[jo] = pv;
-    }
+    write_outputs<16>(a, vr, post, hs, lane);
     const uint64_t b1 = ballot((fl & FLAG_MIN_ZERO) != 0);
     if (lane == 0) {
       a.iters[hs] = iters;
