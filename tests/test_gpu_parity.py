@@ -112,6 +112,10 @@ def _channel(Hx, Hz, p, B, seed):
     ("LP04_0", "F", "BP", 0.1, 100, 512),         # BP team kernel, row degree 7
     ("LP118_0", "S", "MS", 0.05, 3, 256),
     ("T", "F", "MS", 0.05, 50, 1024),
+    ("LP118_2", "L", "MS", None, 50, 512),        # layered MS, fixed work (50 iterations)
+    ("LP118_0", "L", "MS", None, 50, 512),
+    ("LP04_0", "L", "MS", 0.08, 50, 1024),        # layered MS, row degree 7
+    ("LP118_2", "S", "MS", 0.05, 4, 256),         # serial schedule: 450 one-row layers
 ])
 def test_kernel_matches_oracle_batches(dec, code, sched, algo, p, max_iter, B):
     from oracle import oracle
@@ -196,3 +200,4 @@ def test_decode_batch_into_preallocated_buffers(dec):
     bad = dec.DecodeResult(out.ehat[:, :-1], out.iters, None, out.flags)
     with pytest.raises(ValueError):
         dec.decode_batch(Hz, syn, 0.05 / 3, 50, algo="MS", out=bad)
+

@@ -22,8 +22,8 @@ def main():
     for code, dec, sched, osd, it in runs:
         Hx, Hz = codes.load_code(code)
         for p in (0.01, 0.02, 0.05, 0.1):
-            simulator.simulate_p(Hx, Hz, p, shots=1 << 18, decType=dec, decIterations=it,
-                                 decSchedule=sched, OSDorder=osd, rngSeed=1, verbose=False)  # warm-up
+            simulator.simulate_p(Hx, Hz, p, shots=shots, decType=dec, decIterations=it,
+                                 decSchedule=sched, OSDorder=osd, rngSeed=2, verbose=False)  # warm-up: same batches (sizes every pinned slot)
             t0 = time.perf_counter()
             r = simulator.simulate_p(Hx, Hz, p, shots=shots, decType=dec, decIterations=it,
                                      decSchedule=sched, OSDorder=osd, rngSeed=1,
