@@ -208,6 +208,7 @@ struct qldpc_schedule {
   const qldpc_code* code = nullptr;
   bool layered = false;
   int n_layers = 0;
+  int median_rows = 0;        // rows of the median layer (layered MS lanes-per-check choice)
   std::vector<uint8_t> blob;  // LDS image of the graph tables
   // layered MS, uniform degree: layer-ordered tables (ms_layered_kernel)
   std::vector<uint8_t> lblob;
@@ -328,6 +329,12 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
       }
       lay_ptr[l + 1] = (uint16_t)lay_rows.size();
       adj_ptr[l + 1] = (uint16_t)adj_vars.size();
+    }
+    {
+      std::vector<int> rows(n_layers);
+      for (int l = 0; l < n_layers; ++l) rows[l] = (int)layers[l].size();
+      std::sort(rows.begin(), rows.end());
+      s->median_rows = n_layers ? rows[n_layers / 2] : 0;
     }
     s->off_vn_chk = put(s->blob, vn_chk);
     s->off_lay_ptr = put(s->blob, lay_ptr);
@@ -480,7 +487,11 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   bool use_lblob = false;
   if (!cfg.kernel && algo == QLDPC_ALGO_MS && s->layered && dc > 0 && !s->lblob.empty() &&
       !getenv("QLDPC_NO_LAYERED_FAST")) {
-    cfg.kernel = qldpc::select_ms_layered_kernel(dc);
+    // lanes per check: 8 for one- or two-row layers (serial schedules), else
+    // one (interleaved A/B, DESIGN.md §3.2: wider groups lost on 7-60-row layers)
+    int g = s->median_rows <= 2 ? 8 : 1;
+    if (const char* ev = getenv("QLDPC_MS_LANES_PER_CHECK")) g = atoi(ev);
+    cfg.kernel = qldpc::select_ms_layered_kernel(dc, g);
     use_lblob = cfg.kernel != nullptr;
   }
   cfg.lblob = use_lblob;

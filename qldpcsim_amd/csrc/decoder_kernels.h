@@ -43,9 +43,10 @@ const void* select_kernel(int algo, bool layered, int dc);
 // flooding MS, uniform row degree: global tables (fblob), LDS = wave state only
 const void* select_ms_flood_kernel(int dc, int kc);  // nullptr if no instantiation fits
 int ms_flood_max_waves(int kc);                      // waves per workgroup it was compiled for
-const void* select_ms_layered_kernel(int dc);
+// layered MS, uniform row degree 7/8, G = 1/2/4/8 lanes per check (layer-table blob)
+const void* select_ms_layered_kernel(int dc, int g);
 // BP, uniform row degree 7/8: one team of W waves per half-shot, edge-parallel check nodes
-const void* select_bp_team_kernel(bool layered, int dc, int w);                // layered MS, uniform degree (blob: layer tables)                               // waves per workgroup it was compiled for
+const void* select_bp_team_kernel(bool layered, int dc, int w);
 hipError_t launch_decode(const void* kernel, const DecodeArgs& args, int grid, int block,
                          int lds_bytes, hipStream_t stream);
 hipError_t configure_kernel(const void* kernel, int lds_bytes);

@@ -1036,6 +1036,100 @@ ms_flood_kernel(DecodeArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Check node of the layered kernel with G lanes per check (G = 1, 2, 4, 8):
+// lane `sub` of a group owns the EPL = 8 / G consecutive edges sub*EPL ..
+// of its check. Layers are short (LP118_2: 30 rows, LP118_0: 16, serial: 1),
+// so one lane per check left most of the wave idle while it walked all DC
+// edges; with G lanes the per-lane chain is EPL edges long and a wave covers
+// 64 / G checks per pass. Per lane: min1/min2 of its |v| by the tournament,
+// then merged across the group with DPP lane swaps (quad xor 1, quad xor 2,
+// half-row mirror) by (l1,h1)+(l2,h2) -> (min(l1,l2), min(max(l1,l2),
+// min(h1,h2))); min / max are exact, so the group ends with the reference's
+// two values (decoders.py:160-166) whatever the order. The sign product is
+// the XOR of the group's sign words over the same swaps. Missing edges (k >=
+// DC) read post[0], count as |v| = inf and write nothing.
+// ---------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double x) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, x);
+  return __builtin_bit_cast(double, ((uint64_t)dpp_u32<CTRL>((uint32_t)(u >> 32)) << 32) | dpp_u32<CTRL>((uint32_t)u));
+}
+constexpr int kDppQuadXor1 = 0xB1;     // quad_perm [1,0,3,2]
+constexpr int kDppQuadXor2 = 0x4E;     // quad_perm [2,3,0,1]
+constexpr int kDppHalfMirror = 0x141;  // row_half_mirror: lane i <-> 7-i within 8
+
+template <int CTRL>
+__device__ __forceinline__ void group_merge(double& lo, double& hi, uint32_t& sh) {
+  const double olo = dpp_f64<CTRL>(lo), ohi = dpp_f64<CTRL>(hi);
+  sh ^= dpp_u32<CTRL>(sh);
+  const double nlo = vmin_f64(lo, olo);
+  hi = vmin_f64(vmax_f64(lo, olo), vmin_f64(hi, ohi));
+  lo = nlo;
+}
+
+template <int DC, int G>
+__device__ __forceinline__ void cn_ms_split(const DecodeArgs& a, const uint32_t* trow, int sub, bool live,
+                                            uint32_t synb, bool first, uint32_t post_b, uint32_t c2v_b,
+                                            int& fl) {
+  constexpr int EPL = 8 / G;
+  uint32_t t[EPL];
+  if constexpr (EPL == 8) {
+    load_row8(trow, t);
+  } else if constexpr (EPL == 4) {
+    const uint4 w = *(const uint4*)(trow + 4 * sub);
+    t[0] = w.x; t[1] = w.y; t[2] = w.z; t[3] = w.w;
+  } else if constexpr (EPL == 2) {
+    const uint2 w = *(const uint2*)(trow + 2 * sub);
+    t[0] = w.x; t[1] = w.y;
+  } else {
+    t[0] = trow[sub];
+  }
+  bool ek[EPL];
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) ek[i] = live && (DC == 8 || EPL * sub + i < DC);
+  double v[EPL];
+  uint32_t hv[EPL];
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    if (first) {
+      v[i] = (double)a.L32;                                       // (:148-149)
+    } else {
+      const double pj = *QLDPC_LDS(const double, post_b + (t[i] & 0xffffu));
+      const float cv = *QLDPC_LDS(const float, c2v_b + (t[i] >> 16));
+      v[i] = pj - (double)cv;                                     // v2c = post - c2v (:177)
+    }
+    hv[i] = ek[i] ? hi_word(v[i]) : 0u;
+  }
+  double av[EPL];
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) av[i] = ek[i] ? v[i] : __builtin_inf();
+  double lo, hi;
+  min12_tree<EPL>(av, lo, hi);
+  uint32_t sh = xor_tree<EPL>(hv);                                // np.sign product (:157-159)
+  if constexpr (G >= 2) group_merge<kDppQuadXor1>(lo, hi, sh);
+  if constexpr (G >= 4) group_merge<kDppQuadXor2>(lo, hi, sh);
+  if constexpr (G >= 8) group_merge<kDppHalfMirror>(lo, hi, sh);
+  double m1 = lo, m2 = hi;
+  if (__builtin_expect(ballot(live && ((lo == 0.0) | (hi == __builtin_inf()))) != 0, 0)) {
+    m1 = __builtin_isinf(lo) ? 0.0 : lo;                          // (:165)
+    m2 = __builtin_isinf(hi) ? 0.0 : hi;                          // (:166)
+    if (m1 == 0.0 && live) fl |= FLAG_MIN_ZERO;
+  }
+  const uint32_t npm = ((sh >> 31) ^ synb) << 31;
+  const uint32_t c1n = __builtin_bit_cast(uint32_t, (float)(a.beta * m1)) ^ npm;
+  const uint32_t c2n = __builtin_bit_cast(uint32_t, (float)(a.beta * m2)) ^ npm;
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    const uint32_t c = (__builtin_fabs(v[i]) == lo) ? c2n : c1n;   // (:167-168)
+    if (ek[i]) *QLDPC_LDS(uint32_t, c2v_b + (t[i] >> 16)) = c ^ (hv[i] & 0x80000000u);
+  }
+}
+
 
 // ---------------------------------------------------------------------------
 // Layered / serial min-sum for uniform-degree codes (decoders.py:153-177 with
@@ -1046,7 +1140,60 @@ ms_flood_kernel(DecodeArgs a) {
 // (variable, csc start | degree) so every phase is one dependent LDS hop
 // shorter than decode_kernel<MS, true, DC>.
 // ---------------------------------------------------------------------------
-template <int DC>
+// Variable-node pass of one layer (decoders.py:172-174 over the layer's
+// adjacent variables) for a wave-uniform degree bound K: two 64-variable
+// chunks per trip with every LDS read of both issued before the sums (the
+// chunks' variables are distinct, so their post writes never alias the other
+// chunk's reads), then the parity toggles of flipped hard decisions. Measured
+// (interleaved A/B): LP118_2 MS-L -16..-18 %, LP118_0 -9 %; toggles with the
+// check ids hoisted and one predicated atomic per term were slower than this
+// per-lane loop (only flipped lanes iterate, over their own degree).
+template <int K>
+__device__ __forceinline__ void vn_layer(const uint32_t* adj_info, const uint16_t* vn_chk, double* post,
+                                         const float* c2v, uint32_t* parw, int v0, int v1, int lane,
+                                         double L) {
+  for (int qb = v0; qb < v1; qb += 128) {
+    uint32_t info[2];
+    bool in[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int q = qb + 64 * h + lane;
+      in[h] = q < v1;
+      info[h] = adj_info[in[h] ? q : v0];
+    }
+    double old[2];
+    float x[2][K];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      old[h] = post[info[h] >> 21];
+      const float* c = c2v + (info[h] & 0xffffu);
+#pragma unroll
+      for (int t = 0; t < K; ++t) x[h][t] = c[t];          // c2v padded by 8 floats
+    }
+    bool flip[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int d = (int)((info[h] >> 16) & 31u);
+      float s = 0.0f;                                     // sequential, ascending check (:172)
+#pragma unroll
+      for (int t = 0; t < K; ++t) s += (t < d) ? x[h][t] : 0.0f;
+      const double nw = L + (double)s;                    // (:173)
+      if (in[h]) post[info[h] >> 21] = nw;
+      flip[h] = in[h] && ((old[h] < 0.0) != (nw < 0.0));  // hard decision flipped (:174)
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (flip[h]) {
+        for (int p = (int)(info[h] & 0xffffu), pe = p + (int)((info[h] >> 16) & 31u); p < pe; ++p) {
+          const int c = vn_chk[p];
+          atomicXor(&parw[c >> 5], 1u << (c & 31));
+        }
+      }
+    }
+  }
+}
+
+template <int DC, int G>
 __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   {
@@ -1072,6 +1219,7 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
   float* c2v = (float*)c2v_b;
   uint32_t* synw = (uint32_t*)(ws + a.off_synw);
   uint32_t* parw = (uint32_t*)(ws + a.off_parw);
+  const uint32_t post_b = lds_addr(post);
   const int m = a.m, n = a.n;
   const int nwords = (m + 31) >> 5;
   VinvRegs<16> vr;                                             // n <= 1024 in registers
@@ -1095,16 +1243,29 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
     for (int it = 0; it < a.max_iter && !conv; ++it) {
       for (int l = 0; l < a.n_layers; ++l) {
         const int q0 = lay_ptr[l], q1 = lay_ptr[l + 1];
-        for (int q = q0 + lane; q < q1; q += 64) {
-          uint32_t t[1][8];
-          load_row8(ltab + q * 8, t[0]);
-          const int c = lrow[q];
-          const uint32_t sb[1] = {(synw[c >> 5] >> (c & 31)) & 1u};
-          const bool live[1] = {true};
-          if (first)
-            (void)cn_ms_uniform<DC, true, 1>(a, t, sb, live, (const unsigned char*)post, c2v_b, fl);
-          else
-            (void)cn_ms_uniform<DC, false, 1>(a, t, sb, live, (const unsigned char*)post, c2v_b, fl);
+        if constexpr (G == 1) {
+          for (int q = q0 + lane; q < q1; q += 64) {
+            uint32_t t[1][8];
+            load_row8(ltab + q * 8, t[0]);
+            const int c = lrow[q];
+            const uint32_t sb[1] = {(synw[c >> 5] >> (c & 31)) & 1u};
+            const bool live[1] = {true};
+            if (first)
+              (void)cn_ms_uniform<DC, true, 1>(a, t, sb, live, (const unsigned char*)post, c2v_b, fl);
+            else
+              (void)cn_ms_uniform<DC, false, 1>(a, t, sb, live, (const unsigned char*)post, c2v_b, fl);
+          }
+        } else {
+          // G lanes per check, 64 / G checks per pass; every lane takes part
+          // in the group swaps, so the loop runs wave-uniformly
+          for (int qb = q0; qb < q1; qb += 64 / G) {
+            const int q = qb + lane / G;
+            const bool live = q < q1;
+            const int qs = live ? q : q0;
+            const int c = lrow[qs];
+            const uint32_t sb = (synw[c >> 5] >> (c & 31)) & 1u;
+            cn_ms_split<DC, G>(a, ltab + qs * 8, lane & (G - 1), live, sb, first, post_b, lds_addr(c2v_b), fl);
+          }
         }
         first = false;
         wave_sync();
@@ -1112,19 +1273,26 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
         // other columns are unchanged, so this equals the full recompute)
         const int v0 = adj_ptr[l], v1 = adj_ptr[l + 1];
         const int dmax = __builtin_amdgcn_readfirstlane((int)adj_dmax[l]);
-        for (int q = v0 + lane; q < v1; q += 64) {
-          const uint32_t info = adj_info[q];
-          const int j = (int)(info >> 21), d = (int)((info >> 16) & 31u);
-          const double old = post[j];
-          const float s = ms_colsum_sw(c2v + (info & 0xffffu), d, dmax);
-          const double nw = L + (double)s;
-          post[j] = nw;
-          if ((old < 0.0) != (nw < 0.0)) {                       // hard decision flipped
-            for (int p = (int)(info & 0xffffu), pe = p + d; p < pe; ++p) {
-              const int c = vn_chk[p];
-              atomicXor(&parw[c >> 5], 1u << (c & 31));
+        switch (dmax) {
+          case 3: vn_layer<3>(adj_info, vn_chk, post, c2v, parw, v0, v1, lane, L); break;
+          case 4: vn_layer<4>(adj_info, vn_chk, post, c2v, parw, v0, v1, lane, L); break;
+          case 5: vn_layer<5>(adj_info, vn_chk, post, c2v, parw, v0, v1, lane, L); break;
+          case 6: vn_layer<6>(adj_info, vn_chk, post, c2v, parw, v0, v1, lane, L); break;
+          default:
+            for (int q = v0 + lane; q < v1; q += 64) {
+              const uint32_t info = adj_info[q];
+              const int j = (int)(info >> 21), d = (int)((info >> 16) & 31u);
+              const double old = post[j];
+              const float s = ms_colsum_sw(c2v + (info & 0xffffu), d, dmax);
+              const double nw = L + (double)s;
+              post[j] = nw;
+              if ((old < 0.0) != (nw < 0.0)) {                   // hard decision flipped
+                for (int p = (int)(info & 0xffffu), pe = p + d; p < pe; ++p) {
+                  const int c = vn_chk[p];
+                  atomicXor(&parw[c >> 5], 1u << (c & 31));
+                }
+              }
             }
-          }
         }
         wave_sync();
         uint32_t un = 0;                                         // stop test (:175-176)
@@ -1406,9 +1574,11 @@ const void* select_bp_team_kernel(bool layered, int dc, int w) {
   return nullptr;
 }
 
-const void* select_ms_layered_kernel(int dc) {
-  if (dc == 7) return (const void*)&ms_layered_kernel<7>;
-  if (dc == 8) return (const void*)&ms_layered_kernel<8>;
+const void* select_ms_layered_kernel(int dc, int g) {
+#define QLDPC_MSL(D, Gn) if (dc == D && g == Gn) return (const void*)&ms_layered_kernel<D, Gn>;
+  QLDPC_MSL(7, 1) QLDPC_MSL(8, 1) QLDPC_MSL(7, 2) QLDPC_MSL(8, 2)
+  QLDPC_MSL(7, 4) QLDPC_MSL(8, 4) QLDPC_MSL(7, 8) QLDPC_MSL(8, 8)
+#undef QLDPC_MSL
   return nullptr;
 }
 

@@ -201,3 +201,35 @@ def test_decode_batch_into_preallocated_buffers(dec):
     with pytest.raises(ValueError):
         dec.decode_batch(Hz, syn, 0.05 / 3, 50, algo="MS", out=bad)
 
+
+
+@pytest.mark.parametrize("kernel", ["G1", "G2", "G4", "G8", "generic"])
+def test_ms_layered_kernels_match_oracle(dec, kernel, monkeypatch):
+    """ms_layered_kernel at every lanes-per-check width G (QLDPC_MS_LANES_PER_CHECK;
+    the default picks one from the median layer) and the generic decode kernel
+    (QLDPC_NO_LAYERED_FAST) against the oracle, bit for bit, on LP118_2 with
+    fixed-work and channel syndromes: G changes which lanes own which edges,
+    never the arithmetic."""
+    from oracle import oracle
+    from qldpcsim_amd import _lib, codes, schedule
+    Hx, Hz = codes.load_code("LP118_2")
+    if kernel == "generic":
+        monkeypatch.setenv("QLDPC_NO_LAYERED_FAST", "1")
+    else:
+        monkeypatch.setenv("QLDPC_MS_LANES_PER_CHECK", kernel[1:])
+    lx, _ = schedule.select_layers(Hx, Hz, "L")
+    lp, lr = schedule.pack_layers(lx, Hz.shape[0])
+    rng = np.random.default_rng(11)
+    syn = np.concatenate([rng.integers(0, 2, (128, Hz.shape[0]), dtype=np.uint8),
+                          _channel(Hx, Hz, 0.06, 256, 5)[0]])
+    code = _lib.code_for(Hz)
+    code._sched.clear()                  # launch configs read the env once per schedule
+    try:
+        r = dec.decode_batch(Hz, syn, 0.06 / 3, 30, algo="MS", want_post=True, layer_ptr=lp, layer_rows=lr)
+    finally:
+        code._sched.clear()
+    e, it, post, fl = oracle.decode_batch("MS", Hz, syn, 0.06 / 3, 30, lp, lr)
+    np.testing.assert_array_equal(r.iters, it)
+    np.testing.assert_array_equal(r.ehat, e)
+    np.testing.assert_array_equal(r.post.view(np.uint64), post.view(np.uint64))
+    np.testing.assert_array_equal((r.flags & 2) != 0, (fl & 1) != 0)
