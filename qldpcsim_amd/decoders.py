@@ -146,10 +146,22 @@ def osd_perms(post, nthreads=None):
         return np.zeros((0, post.shape[1]), np.int32)
 
     def one(P):
-        sat = np.where(np.abs(P) < 100.0, P, 100.0 * np.sign(P))
-        prob = 1. / (1. + np.exp(sat))
-        rel = np.where(prob > 0.5, prob, 1 - prob)
-        return np.argsort(rel, axis=1).astype(np.int32)
+        # the reference's reliability, element for element (tests pin the bits):
+        #   np.where(|P| < 100, P, 100 sign P)  ==  np.clip(P, -100, 100)
+        #   1 / (1 + exp(sat))                  (same ufuncs, in place)
+        #   np.where(prob > 0.5, prob, 1-prob)  ==  np.maximum(prob, 1-prob)
+        #     (1 - prob is exact for prob > 0.5, and >= 0.5 >= prob otherwise)
+        # 4x fewer passes over the block than the literal form, then NumPy's own
+        # argsort decides the order (and its ties) exactly as the reference's.
+        out = np.empty((P.shape[0], P.shape[1]), np.int32)
+        for r0 in range(0, P.shape[0], 64):          # cache-sized row blocks
+            t = np.clip(P[r0:r0 + 64], -100.0, 100.0)
+            np.exp(t, out=t)
+            np.add(t, 1.0, out=t)
+            np.divide(1.0, t, out=t)
+            np.maximum(t, np.subtract(1.0, t), out=t)
+            out[r0:r0 + 64] = np.argsort(t, axis=1)
+        return out
 
     import os
     nthreads = nthreads or min(16, os.cpu_count() or 1)
