@@ -346,7 +346,7 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
       for (size_t q = 0; q < lay_rows.size(); ++q) {
         const int r = lay_rows[q];
         for (int e = code->row_ptr[r], k = 0; e < code->row_ptr[r + 1]; ++e, ++k)
-          ltab[8 * q + k] = ((uint32_t)(4 * code->edge_pos[e]) << 16) | (uint32_t)(8 * code->vinv[code->col_idx[e]]);
+          ltab[8 * q + k] = ((uint32_t)(4 * code->edge_pos[e]) << 16) | (uint32_t)(4 * code->vinv[code->col_idx[e]]);
       }
       std::vector<uint8_t> adj_dmax(std::max(n_layers, 1), 0);
       for (int l = 0; l < n_layers; ++l)
@@ -438,8 +438,8 @@ extern "C" int qldpc_schedule_destroy(qldpc_schedule* s) {
 
 // per-wave state slice: post f64[n] | c2v (f32|f64)[E] | syn words | parity words
 static void wave_layout(const qldpc_code* c, bool layered, int algo, int* bytes, int* off_c2v,
-                        int* off_synw, int* off_parw) {
-  int off = align16(8 * c->n);
+                        int* off_synw, int* off_parw, bool colsum_f32 = false) {
+  int off = align16((colsum_f32 ? 4 : 8) * c->n);   // post f64, or ms_layered_kernel's float32 sums
   *off_c2v = off;
   off = align16(off + (algo == QLDPC_ALGO_MS ? 4 : 8) * (c->E + 8));  // +8: VN over-read pad
   const int words = 2 * ((c->m + 63) / 64);
@@ -510,7 +510,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   cfg.team = team;
   if (!cfg.kernel) cfg.kernel = qldpc::select_kernel(algo, s->layered, dc);
   int off_c2v, off_synw, off_parw, off_red;
-  wave_layout(c, s->layered, algo, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw);
+  wave_layout(c, s->layered, algo, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw, use_lblob);
   if (team) team_layout(c, team, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw, &off_red);
   int max_lds = 0, dev = 0;
   HIP_TRY(hipGetDevice(&dev));
@@ -650,7 +650,7 @@ extern "C" int qldpc_decode_device(const qldpc_code* code, const qldpc_schedule*
   a.off_adj_ptr = sched->off_adj_ptr;
   a.off_adj_vars = sched->off_adj_vars;
   a.off_chunk_dmax = sched->off_chunk_dmax;
-  wave_layout(code, sched->layered, algo, &a.wave_bytes, &a.off_c2v, &a.off_synw, &a.off_parw);
+  wave_layout(code, sched->layered, algo, &a.wave_bytes, &a.off_c2v, &a.off_synw, &a.off_parw, cfg->lblob);
   if (cfg->lblob) {  // ms_layered_kernel's blob: field mapping documented in the kernel
     a.blob = sched->d_lblob;
     a.blob_bytes = (int)sched->lblob.size();

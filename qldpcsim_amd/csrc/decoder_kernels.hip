@@ -1099,7 +1099,9 @@ __device__ __forceinline__ void cn_ms_split(const DecodeArgs& a, const uint32_t*
     if (first) {
       v[i] = (double)a.L32;                                       // (:148-149)
     } else {
-      const double pj = *QLDPC_LDS(const double, post_b + (t[i] & 0xffffu));
+      // post_j = L + (f64)S_j rebuilt from the float32 column sum (exact: the
+      // value the reference stores, decoders.py:173)
+      const double pj = a.L + (double)*QLDPC_LDS(const float, post_b + (t[i] & 0xffffu));
       const float cv = *QLDPC_LDS(const float, c2v_b + (t[i] >> 16));
       v[i] = pj - (double)cv;                                     // v2c = post - c2v (:177)
     }
@@ -1149,7 +1151,7 @@ __device__ __forceinline__ void cn_ms_split(const DecodeArgs& a, const uint32_t*
 // check ids hoisted and one predicated atomic per term were slower than this
 // per-lane loop (only flipped lanes iterate, over their own degree).
 template <int K>
-__device__ __forceinline__ void vn_layer(const uint32_t* adj_info, const uint16_t* vn_chk, double* post,
+__device__ __forceinline__ void vn_layer(const uint32_t* adj_info, const uint16_t* vn_chk, float* colS,
                                          const float* c2v, uint32_t* parw, int v0, int v1, int lane,
                                          double L) {
   for (int qb = v0; qb < v1; qb += 128) {
@@ -1165,7 +1167,7 @@ __device__ __forceinline__ void vn_layer(const uint32_t* adj_info, const uint16_
     float x[2][K];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      old[h] = post[info[h] >> 21];
+      old[h] = L + (double)colS[info[h] >> 21];          // post before this layer
       const float* c = c2v + (info[h] & 0xffffu);
 #pragma unroll
       for (int t = 0; t < K; ++t) x[h][t] = c[t];          // c2v padded by 8 floats
@@ -1178,7 +1180,7 @@ __device__ __forceinline__ void vn_layer(const uint32_t* adj_info, const uint16_
 #pragma unroll
       for (int t = 0; t < K; ++t) s += (t < d) ? x[h][t] : 0.0f;
       const double nw = L + (double)s;                    // (:173)
-      if (in[h]) post[info[h] >> 21] = nw;
+      if (in[h]) colS[info[h] >> 21] = s;
       flip[h] = in[h] && ((old[h] < 0.0) != (nw < 0.0));  // hard decision flipped (:174)
     }
 #pragma unroll
@@ -1214,12 +1216,14 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
   const int wid = threadIdx.x >> 6;
   const int waves = blockDim.x >> 6;
   unsigned char* ws = lds + a.blob_bytes + wid * a.wave_bytes;
-  double* post = (double*)ws;
+  // the slice keeps the float32 column sums S (post = L + (f64)S is rebuilt
+  // where it is read): 4 n bytes instead of 8 n, so a CU holds more waves
+  float* colS = (float*)ws;
   unsigned char* c2v_b = ws + a.off_c2v;
   float* c2v = (float*)c2v_b;
   uint32_t* synw = (uint32_t*)(ws + a.off_synw);
   uint32_t* parw = (uint32_t*)(ws + a.off_parw);
-  const uint32_t post_b = lds_addr(post);
+  const uint32_t post_b = lds_addr(colS), c2v_a = lds_addr(c2v_b);
   const int m = a.m, n = a.n;
   const int nwords = (m + 31) >> 5;
   VinvRegs<16> vr;                                             // n <= 1024 in registers
@@ -1234,7 +1238,7 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
     bool conv = false;
     const double L = a.L;
     load_syndrome_bits<8>(syn, m, synw, lane);
-    for (int j = lane; j < n; j += 64) post[j] = L;             // v2c = L, c2v = 0 (:148-150)
+    for (int j = lane; j < n; j += 64) colS[j] = 0.0f;          // post = L, c2v = 0 (:148-150)
     for (int p = lane; p < a.E; p += 64) c2v[p] = 0.0f;
     for (int c0 = 0; c0 < m; c0 += 64)
       store_bits64(parw, c0, (c0 + lane < m) && (L < 0.0) && (DC & 1), lane);
@@ -1250,10 +1254,19 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
             const int c = lrow[q];
             const uint32_t sb[1] = {(synw[c >> 5] >> (c & 31)) & 1u};
             const bool live[1] = {true};
-            if (first)
-              (void)cn_ms_uniform<DC, true, 1>(a, t, sb, live, (const unsigned char*)post, c2v_b, fl);
-            else
-              (void)cn_ms_uniform<DC, false, 1>(a, t, sb, live, (const unsigned char*)post, c2v_b, fl);
+            if (first) {
+              (void)cn_ms_uniform<DC, true, 1>(a, t, sb, live, (const unsigned char*)colS, c2v_b, fl);
+            } else {
+              CnLoad<DC> Ld;
+              uint32_t ca[8];
+#pragma unroll
+              for (int k = 0; k < DC; ++k) {
+                ca[k] = c2v_a + (t[0][k] >> 16);
+                Ld.pj[k] = a.L + (double)*QLDPC_LDS(const float, post_b + (t[0][k] & 0xffffu));   // (:173)
+                Ld.cv[k] = *QLDPC_LDS(const float, ca[k]);
+              }
+              (void)cn_ms_compute<DC>(a, Ld, ca, sb[0], 1u, fl);
+            }
           }
         } else {
           // G lanes per check, 64 / G checks per pass; every lane takes part
@@ -1264,7 +1277,7 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
             const int qs = live ? q : q0;
             const int c = lrow[qs];
             const uint32_t sb = (synw[c >> 5] >> (c & 31)) & 1u;
-            cn_ms_split<DC, G>(a, ltab + qs * 8, lane & (G - 1), live, sb, first, post_b, lds_addr(c2v_b), fl);
+            cn_ms_split<DC, G>(a, ltab + qs * 8, lane & (G - 1), live, sb, first, post_b, c2v_a, fl);
           }
         }
         first = false;
@@ -1274,18 +1287,18 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
         const int v0 = adj_ptr[l], v1 = adj_ptr[l + 1];
         const int dmax = __builtin_amdgcn_readfirstlane((int)adj_dmax[l]);
         switch (dmax) {
-          case 3: vn_layer<3>(adj_info, vn_chk, post, c2v, parw, v0, v1, lane, L); break;
-          case 4: vn_layer<4>(adj_info, vn_chk, post, c2v, parw, v0, v1, lane, L); break;
-          case 5: vn_layer<5>(adj_info, vn_chk, post, c2v, parw, v0, v1, lane, L); break;
-          case 6: vn_layer<6>(adj_info, vn_chk, post, c2v, parw, v0, v1, lane, L); break;
+          case 3: vn_layer<3>(adj_info, vn_chk, colS, c2v, parw, v0, v1, lane, L); break;
+          case 4: vn_layer<4>(adj_info, vn_chk, colS, c2v, parw, v0, v1, lane, L); break;
+          case 5: vn_layer<5>(adj_info, vn_chk, colS, c2v, parw, v0, v1, lane, L); break;
+          case 6: vn_layer<6>(adj_info, vn_chk, colS, c2v, parw, v0, v1, lane, L); break;
           default:
             for (int q = v0 + lane; q < v1; q += 64) {
               const uint32_t info = adj_info[q];
               const int j = (int)(info >> 21), d = (int)((info >> 16) & 31u);
-              const double old = post[j];
+              const double old = L + (double)colS[j];
               const float s = ms_colsum_sw(c2v + (info & 0xffffu), d, dmax);
               const double nw = L + (double)s;
-              post[j] = nw;
+              colS[j] = s;
               if ((old < 0.0) != (nw < 0.0)) {                   // hard decision flipped
                 for (int p = (int)(info & 0xffffu), pe = p + d; p < pe; ++p) {
                   const int c = vn_chk[p];
@@ -1304,7 +1317,23 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
         }
       }
     }
-    write_outputs<16>(a, vr, post, hs, lane);
+    {                                                          // ê, posteriors in original order
+      uint8_t* eh = a.ehat + hs * (long long)n;
+      double* po = a.post ? a.post + hs * (long long)n : nullptr;
+      for (int k = 0; k < 16 && 64 * k < n; ++k) {
+        const int jo = 64 * k + lane;
+        if (jo < n) {
+          const double pv = L + (double)colS[n <= 1024 ? vr.get(k) : a.vinv[jo]];
+          eh[jo] = (uint8_t)(pv < 0.0);
+          if (po) po[jo] = pv;
+        }
+      }
+      for (int jo = 1024 + lane; jo < n; jo += 64) {
+        const double pv = L + (double)colS[a.vinv[jo]];
+        eh[jo] = (uint8_t)(pv < 0.0);
+        if (po) po[jo] = pv;
+      }
+    }
     const uint64_t b1 = ballot((fl & FLAG_MIN_ZERO) != 0);
     if (lane == 0) {
       a.iters[hs] = iters;
