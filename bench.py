@@ -1,20 +1,44 @@
 """bench.py — decoded shots/s for qLDPCsim's decode hot path on MI355X.
 
-Workload (BASELINE.json metric "decoded shots/sec (MS 50-iter, LP118_0)"):
-LP118_0, normalized min-sum, flooding, max 50 iterations, fixed-work uniform
-random syndromes (unsatisfiable w.p. >= 255/256, so every decode runs 50
-iterations). One shot = X half (Hz, sy_z) + Z half
-(Hx, sy_x); one step = one batch of `--batch` shots per GPU = two decode
-kernel launches. Syndromes are generated on the device before timing
-(inputs resident in HBM). N>1: one process per GPU (torch.distributed over
-RCCL), shots shard with no data-path collective (weak scaling); the timed
-region is bracketed by barrier + synchronize, the time is the max over ranks.
+Headline workload (BASELINE.json metric "decoded shots/sec (MS 50-iter,
+LP118_0) at 1/2/4/8 GPU"): LP118_0, normalized min-sum, flooding, max 50
+iterations, fixed-work uniform random syndromes (unsatisfiable w.p. >= 255/256,
+so every decode runs 50 iterations). One shot = X half (Hz,
+sy_z) + Z half (Hx, sy_x); one step = one batch of `--batch` shots per GPU =
+two decode kernel launches. Syndromes are generated on the device before
+timing (inputs resident in HBM); output buffers are allocated once.
+
+Multi-GPU (weak scaling, no data-path collective; the reference's serial shot
+loop simulator.py:244 becomes shards of shots): one process per GPU over RCCL.
+  * under torch.distributed.run (WORLD_SIZE set): this process is one rank;
+  * `python bench.py --gpus N` with no WORLD_SIZE: spawns N fresh rank
+    processes itself (the parent never initialises the GPU).
+N larger than the visible devices fails loudly, unless QLDPC_BENCH_BACKEND=gloo
+(rehearsal: ranks share devices). The timed region is bracketed by barrier +
+synchronize; elapsed time is the max over ranks; `value` = all ranks' shots /
+that time.
+
+`roofline` prices the decode kernel against the on-chip unit that binds it
+(DESIGN.md §3.3): VALU issue (one wave64 VALU instruction per SIMD per 4
+cycles — the SQ's quad-cycle accounting — 1024 SIMDs at 2.4 GHz) or the LDS
+array (one cycle per CU per LDS array cycle, 256 CUs at 2.4 GHz). Per-unit
+instruction / LDS-cycle / HBM-byte counts come from a committed rocprofv3
+profile of the same kernel build (profiles/*_roofline.json, matched by kernel
+name and by the hash of the library's device code object), multiplied by this
+run's executed half-shot iterations and divided by this run's kernel time (HIP
+events on the launch stream). The HBM figures (measured PMC bytes, and
+SURVEY.md §8d's algorithmic streaming model) are reported beside it.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+                       [--code C] [--algo MS|BP] [--schedule F|L|S] [--p P] [--iters I]
 """
 import argparse
+import glob
+import hashlib
 import json
 import os
+import socket
+import struct
 import sys
 import time
 
@@ -24,101 +48,232 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "decoded shots/sec (MS 50-iter, LP118_0) at 1/2/4/8 GPU; achieved HBM GB/s"
-HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+CLOCK_GHZ = 2.4                # max engine clock (MI355X_MICROARCH.md)
+SIMDS, CUS = 1024, 256         # 256 CUs x 4 SIMDs
+VALU_CYCLES = 4                # SQ accounting: one wave64 VALU instruction = one quad-cycle
+REFERENCE_PER_CORE = 2.61      # reference decoders.py, LP118_0 MS-F 50 it fixed work, 1 core
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="GPUs (ranks); default: WORLD_SIZE or 1")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1 << 20, help="shots per GPU per step")
     ap.add_argument("--code", default="LP118_0")
+    ap.add_argument("--algo", default="MS", choices=["MS", "BP"])
+    ap.add_argument("--schedule", default="F", choices=["F", "L", "S"])
+    ap.add_argument("--p", type=float, default=None,
+                    help="depolarizing p for channel syndromes (device sampler); default: "
+                         "uniform random syndromes (fixed work)")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
-                    help="bounded CPU-baseline sample (0 disables)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    return ap.parse_args()
+                    help="bounded CPU-baseline sample per leg (0 disables)")
+    ap.add_argument("--worklog", default=None,
+                    help="write per-launch work (kernel, half-shots, iterations) as JSON (profiling)")
+    return ap.parse_args(argv)
 
 
-def algorithmic_bytes(m, n, E, iters_sum, halves):
-    """SURVEY.md §8d / BASELINE.md: per executed flooding MS iteration of one
-    half-shot 4*(3E + 2n) bytes, plus m + n + 4 bytes of I/O per half-shot."""
-    return 4 * (3 * E + 2 * n) * iters_sum + (m + n + 4) * halves
+# ---------------------------------------------------------------------------
+# host facts
+# ---------------------------------------------------------------------------
+def host_cores():
+    """CPU cores this process may use: the affinity mask, capped by a cgroup
+    CPU quota and by OMP_NUM_THREADS (the GPU box sets it to the box's CPU
+    share). Returns (cores, how)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+        how = ["sched_getaffinity"]
+    except AttributeError:
+        n, how = os.cpu_count() or 1, ["os.cpu_count"]
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            c = max(1, int(float(q) / float(per)))
+            if c < n:
+                n, how = c, how + ["cgroup cpu.max"]
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and 0 < int(omp) < n:
+        n, how = int(omp), how + ["OMP_NUM_THREADS"]
+    return n, " capped by ".join(how)
 
 
-def pmc_traffic(code, batch):
-    """HBM bytes per decode launch from a committed rocprofv3 PMC summary
-    (profiles/*_pmc.json, written by tools/pmc_summary.py), if one matches."""
-    import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), reverse=True):
+def device_code_sha(path):
+    """sha256 of the library's embedded device code (the .hip_fatbin ELF
+    section): unchanged by host-only edits, changed by any kernel edit."""
+    with open(path, "rb") as f:
+        data = f.read()
+    try:
+        shoff, = struct.unpack_from("<Q", data, 0x28)
+        shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+        secs = [struct.unpack_from("<IIQQQQIIQQ", data, shoff + i * shentsize) for i in range(shnum)]
+        stroff = secs[shstrndx][4]
+        for s in secs:
+            nm = data[stroff + s[0]:data.index(b"\0", stroff + s[0])]
+            if nm == b".hip_fatbin":
+                return hashlib.sha256(data[s[4]:s[4] + s[5]]).hexdigest()
+    except (struct.error, ValueError, IndexError):
+        pass
+    return hashlib.sha256(data).hexdigest()
+
+
+def find_profile(kernel, sha):
+    """Newest profiles/*_roofline.json entry for this kernel built from this
+    device code (None if the committed profiles are stale for this build)."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_roofline.json")), reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        if d.get("code") == code and int(d.get("batch", -1)) == batch and "hbm_bytes_per_launch" in d:
-            return float(d["hbm_bytes_per_launch"])
-    return None
-
-
-def onchip_profile(code):
-    """Unit utilisations of the decode kernel from the newest committed SQ
-    counter summary (profiles/*_counters.json, tools/ctr_summary.py --json):
-    the on-chip limiters of an LDS-resident kernel, which HBM bytes cannot show."""
-    import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_counters.json")), reverse=True):
-        try:
-            with open(path) as f:
-                d = json.load(f)
-        except (OSError, ValueError):
+        if d.get("device_code_sha256") != sha:
             continue
-        if d.get("code") == code:
-            keep = ("valu_busy", "lds_busy", "lds_conflict_share", "per_wave_iter_valu",
-                    "per_wave_iter_lds", "per_wave_iter_salu")
-            out = {k: round(d[k], 4) for k in keep if k in d}
-            out["source"] = os.path.relpath(path, ROOT)
-            return out
-    return None
+        for k in d.get("kernels", []):
+            if k.get("kernel") == kernel:
+                return os.path.relpath(path, ROOT), k
+    return None, None
 
 
-def cpu_baseline(code, max_iter, seconds, threads):
-    """The pinned CPU oracle (oracle/qldpc_oracle.c, OpenMP over shots) timed on
-    this host on a bounded sample of the same workload."""
+# ---------------------------------------------------------------------------
+# algorithmic byte model (SURVEY.md §8d) — reported beside the roofline
+# ---------------------------------------------------------------------------
+def algorithmic_bytes_per_iter(H, layer_ptr, layer_rows, word):
+    """Bytes one executed iteration of one half-shot moves under the HBM
+    streaming model: flooding w(3E + 2n); layered sum over layers of
+    w(2E_l + sum_{j in V_l} d_j + 2|V_l|)."""
+    m, n = H.shape
+    E = int(H.sum())
+    if len(layer_ptr) == 2 and layer_ptr[1] == m:
+        return word * (3 * E + 2 * n)
+    deg = H.sum(axis=0)
+    tot = 0
+    for l in range(len(layer_ptr) - 1):
+        rows = layer_rows[layer_ptr[l]:layer_ptr[l + 1]]
+        El = int(H[rows].sum())
+        V = np.flatnonzero(H[rows].any(axis=0))
+        tot += word * (2 * El + int(deg[V].sum()) + 2 * len(V))
+    return tot
+
+
+# ---------------------------------------------------------------------------
+# CPU baselines (rank 0, N = 1): bounded samples of the same workload
+# ---------------------------------------------------------------------------
+def _cpu_syndromes(Hx, Hz, p, B, rng):
+    if p is None:
+        return (rng.integers(0, 2, (B, Hz.shape[0]), dtype=np.uint8),
+                rng.integers(0, 2, (B, Hx.shape[0]), dtype=np.uint8))
+    from qldpcsim_amd.simulator import sample_channel
+    sz, sx, _, _ = sample_channel(Hx, Hz, p, B, rng)
+    return sz, sx
+
+
+def cpu_baseline_port(args, cores):
+    """oracle/qldpc_oracle.c (OpenMP over shots, bit-exact vs the reference's
+    golden vectors) on `cores` threads."""
     from oracle import oracle
-    from qldpcsim_amd import codes
-    Hx, Hz = codes.load_code(code)
+    from qldpcsim_amd import codes, schedule
+    Hx, Hz = codes.load_code(args.code)
+    lx, lz = schedule.select_layers(Hx, Hz, args.schedule)
+    (lpx, lrx), (lpz, lrz) = schedule.pack_layers(lx, Hz.shape[0]), schedule.pack_layers(lz, Hx.shape[0])
+    prior = (0.05 if args.p is None else args.p) / 3
     rng = np.random.default_rng(12345)
-    chunk = 64 * threads
+    chunk = 64 * cores
     shots = 0
     t0 = time.perf_counter()
     while True:
-        sz = rng.integers(0, 2, (chunk, Hz.shape[0]), dtype=np.uint8)
-        sx = rng.integers(0, 2, (chunk, Hx.shape[0]), dtype=np.uint8)
-        oracle.decode_batch("MS", Hz, sz, 0.05 / 3, max_iter, want_post=False, nthreads=threads)
-        oracle.decode_batch("MS", Hx, sx, 0.05 / 3, max_iter, want_post=False, nthreads=threads)
+        sz, sx = _cpu_syndromes(Hx, Hz, args.p, chunk, rng)
+        oracle.decode_batch(args.algo, Hz, sz, prior, args.iters, lpx, lrx, want_post=False, nthreads=cores)
+        oracle.decode_batch(args.algo, Hx, sx, prior, args.iters, lpz, lrz, want_post=False, nthreads=cores)
         shots += chunk
         el = time.perf_counter() - t0
-        if el >= seconds:
+        if el >= args.cpu_seconds:
             break
-    return {"value": shots / el, "unit": "shots/s", "cores": threads, "kind": "port",
-            "sample": f"{shots} shots ({code} MS flooding {max_iter} it, uniform random syndromes,"
-                      f" both halves) in {el:.1f} s with oracle/qldpc_oracle.c, {threads} OpenMP threads"}
+    return {"value": shots / el, "unit": "shots/s", "cores": cores, "kind": "port",
+            "sample": f"{shots} shots of the bench workload (both halves) in {el:.1f} s with "
+                      f"oracle/qldpc_oracle.c, {cores} OpenMP threads"}
 
 
-def main():
-    args = parse()
+def _numpy_worker(a):
+    code, sched, p, iters, seconds, seed = a
+    from oracle import numpy_dense
+    from qldpcsim_amd import codes, schedule
+    Hx, Hz = codes.load_code(code)
+    lx, lz = schedule.select_layers(Hx, Hz, sched)
+    dz, dx = numpy_dense.DenseMinSum(Hz), numpy_dense.DenseMinSum(Hx)
+    prior = (0.05 if p is None else p) / 3
+    rng = np.random.default_rng(seed)
+    shots = 0
+    t0 = time.perf_counter()
+    while True:
+        sz, sx = _cpu_syndromes(Hx, Hz, p, 1, rng)
+        dz.decode(sz[0].astype(np.int64), prior, iters, lx)
+        dx.decode(sx[0].astype(np.int64), prior, iters, lz)
+        shots += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            return shots, el
+
+
+def cpu_baseline_numpy(args, cores):
+    """oracle/numpy_dense.py (the reference's dense per-shot structure,
+    bit-exact vs its golden vectors): one process per core, OMP_NUM_THREADS=1."""
+    import multiprocessing as mp
+    old = os.environ.get("OMP_NUM_THREADS")
+    os.environ["OMP_NUM_THREADS"] = "1"
+    try:
+        with mp.get_context("spawn").Pool(cores) as pool:
+            res = pool.map(_numpy_worker, [(args.code, args.schedule, args.p, args.iters,
+                                            args.cpu_seconds, 777 + i) for i in range(cores)])
+    finally:
+        if old is None:
+            os.environ.pop("OMP_NUM_THREADS", None)
+        else:
+            os.environ["OMP_NUM_THREADS"] = old
+    rate = sum(s / e for s, e in res)
+    tot = sum(s for s, _ in res)
+    return {"value": rate, "unit": "shots/s", "cores": cores, "kind": "port",
+            "sample": f"{tot} shots one at a time over {cores} processes, ~{args.cpu_seconds:.0f} s each, "
+                      f"oracle/numpy_dense.py (dense NumPy restatement of decoders.py:147-177)"}
+
+
+def cpu_baselines(args):
+    cores, how = host_cores()
+    legs = [cpu_baseline_port(args, cores)]
+    if args.algo == "MS":
+        legs.append(cpu_baseline_numpy(args, cores))
+    out = dict(legs[0])
+    out["cores_source"] = how
+    out["legs"] = legs
+    if args.code == "LP118_0" and args.algo == "MS" and args.schedule == "F" and args.p is None:
+        out["reference_context"] = {
+            "value": REFERENCE_PER_CORE, "unit": "shots/s/core",
+            "source": "the reference's own decoders.py on this workload, 1 core (BASELINE.md survey run)",
+            "x_cores": REFERENCE_PER_CORE * cores}
+    return out
+
+
+# ---------------------------------------------------------------------------
+# one rank
+# ---------------------------------------------------------------------------
+def run_rank(args, rank, world, local):
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one process per GPU; QLDPC_BENCH_BACKEND=gloo (and more ranks than GPUs,
-    # ranks sharing a device) only to exercise this path on a one-GPU box
     backend = os.environ.get("QLDPC_BENCH_BACKEND", "nccl")
-    local = local % max(1, torch.cuda.device_count())
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    if ndev == 0:
+        raise SystemExit("bench.py: no HIP device visible")
+    if local >= ndev and backend == "nccl":
+        raise SystemExit(f"bench.py: rank {rank} has local rank {local} but only {ndev} device(s) are "
+                         "visible (one GPU per rank; QLDPC_BENCH_BACKEND=gloo to rehearse on shared devices)")
+    cpu = None
+    if world == 1 and rank == 0 and args.cpu_seconds > 0:
+        cpu = cpu_baselines(args)          # before the GPU is touched (spawned pool)
+    dev = torch.device("cuda", local % ndev)
     torch.cuda.set_device(dev)
     if world > 1:
         if backend == "nccl":
@@ -126,35 +281,52 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    from qldpcsim_amd import _lib, codes, decoders
+    from qldpcsim_amd import _lib, codes, decoders, schedule
+    from qldpcsim_amd.simulator import DeviceChannel
     Hx, Hz = codes.load_code(args.code)
     m, n = Hz.shape
     E = int(Hz.sum())
-    assert int(Hx.sum()) == E and Hx.shape == Hz.shape
+    lx, lz = schedule.select_layers(Hx, Hz, args.schedule)
+    lpx, lrx = schedule.pack_layers(lx, Hz.shape[0])       # X half: Hz with Hx's layers
+    lpz, lrz = schedule.pack_layers(lz, Hx.shape[0])       # Z half: Hx with Hz's layers
     B = args.batch
-    g = torch.Generator(device=dev).manual_seed(20251226 + rank)
-    syn_z = torch.randint(0, 2, (B, Hz.shape[0]), dtype=torch.uint8, device=dev, generator=g)
-    syn_x = torch.randint(0, 2, (B, Hx.shape[0]), dtype=torch.uint8, device=dev, generator=g)
-    prior = 0.05 / 3
+    if args.p is None:
+        g = torch.Generator(device=dev).manual_seed(20251226 + rank)
+        syn_z = torch.randint(0, 2, (B, Hz.shape[0]), dtype=torch.uint8, device=dev, generator=g)
+        syn_x = torch.randint(0, 2, (B, Hx.shape[0]), dtype=torch.uint8, device=dev, generator=g)
+        prior = 0.05 / 3
+    else:
+        ch = DeviceChannel(Hx, Hz, dev, seed=20251226 + rank)
+        syn_z, syn_x, _, _ = ch.sample(args.p, B)
+        prior = args.p / 3
+    halves = ((Hz, syn_z, lpx, lrx), (Hx, syn_x, lpz, lrz))
+    want_post = False
 
-    # output buffers allocated once (a step allocates nothing)
-    def buffers():
-        return decoders.DecodeResult(torch.empty((B, n), dtype=torch.uint8, device=dev),
+    def buffers(H):
+        return decoders.DecodeResult(torch.empty((B, H.shape[1]), dtype=torch.uint8, device=dev),
                                      torch.empty(B, dtype=torch.int32, device=dev), None,
                                      torch.empty(B, dtype=torch.int32, device=dev))
-    out_z, out_x = buffers(), buffers()
+    outs = [buffers(H) for H, _, _, _ in halves]
+
+    log = []                                               # per launch: (kernel, half-shots, iters tensor)
+    names = [_lib.kernel_name(H, lp, lr, args.algo, dev.index) for H, _, lp, lr in halves]
 
     def step():
-        rz = decoders.decode_batch(Hz, syn_z, prior, args.iters, algo="MS", out=out_z)
-        rx = decoders.decode_batch(Hx, syn_x, prior, args.iters, algo="MS", out=out_x)
-        return rz, rx
+        res = []
+        for (H, s, lp, lr), o, nm in zip(halves, outs, names):
+            r = decoders.decode_batch(H, s, prior, args.iters, algo=args.algo, out=o, layer_ptr=lp,
+                                      layer_rows=lr, want_post=want_post)
+            res.append(r)
+            if args.worklog:
+                log.append((nm, B, r.iters.sum(dtype=torch.int64)))
+        return res
 
     iters_sum = torch.zeros((), dtype=torch.int64, device=dev)
     for _ in range(args.warmup):
         # the same work as a timed step, including the iteration reduction (the
         # first use of torch's reduce kernel loads its code object: ~0.1 s)
-        rz, rx = step()
-        iters_sum += rz.iters.sum(dtype=torch.int64) + rx.iters.sum(dtype=torch.int64)
+        for r in step():
+            iters_sum += r.iters.sum(dtype=torch.int64)
     torch.cuda.synchronize()
     _lib.timing_enable(True)
     _lib.timing_reset()
@@ -164,8 +336,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        rz, rx = step()
-        iters_sum += rz.iters.sum(dtype=torch.int64) + rx.iters.sum(dtype=torch.int64)
+        for r in step():
+            iters_sum += r.iters.sum(dtype=torch.int64)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -173,19 +345,31 @@ def main():
     kern_ms, launches = _lib.timing_read()
     _lib.timing_enable(False)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tdev = dev if backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    if args.worklog and rank == 0:
+        with open(args.worklog, "w") as f:
+            json.dump({"launches": [{"kernel": nm, "half_shots": b, "iters": int(it.item())}
+                                    for nm, b, it in log]}, f)
     total_shots = B * args.steps * world
     value = total_shots / elapsed
 
-    halves = 2 * B * args.steps
+    halves_timed = 2 * B * args.steps
     its = int(iters_sum.item())
-    algo_bytes_launch = algorithmic_bytes(m, n, E, its, halves) / launches
     avg_launch_s = kern_ms / 1e3 / launches
-    achieved = algo_bytes_launch / avg_launch_s / 1e9
-    traffic = pmc_traffic(args.code, B)
+    hs_per_launch = halves_timed / launches
+    it_per_launch = its / launches
+    word = 4 if args.algo == "MS" else 8
+    algo_bytes = sum(algorithmic_bytes_per_iter(H.astype(np.int64), lp, lr, word) for H, _, lp, lr in halves) / 2
+    algo_launch = algo_bytes * it_per_launch + (m + n + 4) * hs_per_launch
+    roof = roofline(names, avg_launch_s, hs_per_launch, it_per_launch, algo_launch, launches)
 
+    sched_name = {"F": "flooding", "L": "layered", "S": "serial"}[args.schedule]
+    algo_name = "normalized min-sum (beta 0.75)" if args.algo == "MS" else "sum-product BP"
+    synd = "fixed-work uniform random syndromes (SURVEY.md 8d(i))" if args.p is None else \
+        f"depolarizing channel p={args.p} (device Philox sampler)"
     out = {
         "metric": METRIC,
         "value": value,
@@ -197,41 +381,124 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32+f64",
+        "dtype": "f32+f64" if args.algo == "MS" else "f64",
         "data": "synthetic",
         "config": {
-            "workload": f"{args.code} normalized min-sum (beta 0.75), flooding, max {args.iters} "
-                        "iterations, fixed-work uniform random syndromes (SURVEY.md 8d(i)); "
+            "workload": f"{args.code} {algo_name}, {sched_name}, max {args.iters} iterations, {synd}; "
                         "1 shot = X half + Z half",
-            "code": args.code, "m": m, "n": n, "edges": E,
+            "code": args.code, "algo": args.algo, "schedule": args.schedule, "p": args.p,
+            "m": m, "n": n, "edges": E,
             "shots_per_gpu_per_step": B, "global_batch": B * world,
-            "avg_iterations": its / halves,
-            "parallelism": f"shots sharded over {world} GPU(s), no data-path collective",
+            "avg_iterations": its / halves_timed,
+            "parallelism": f"shots sharded over {world} GPU(s) (one process per GPU, {backend}), "
+                           "no data-path collective",
         },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic,
-            "note": "achieved = SURVEY 8d algorithmic bytes (4*(3E+2n) per executed half-shot "
-                    "iteration + m+n+4 I/O) / mean decode-kernel duration (HIP events on the launch "
-                    "stream). Message state is LDS-resident, so real HBM traffic (traffic) is "
-                    "far below the algorithmic model; the kernel's actual limiters are on chip "
-                    "(onchip: VALU / LDS busy fractions from rocprofv3 SQ counters).",
-            "kernel_ms_per_launch": avg_launch_s * 1e3,
-            "launches": launches,
-            "onchip": onchip_profile(args.code),
-        },
+        "roofline": roof,
     }
-    if world == 1 and rank == 0 and args.cpu_seconds > 0:
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-        out["cpu_baseline"] = cpu_baseline(args.code, args.iters, args.cpu_seconds, threads)
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def roofline(names, t_launch, hs_launch, it_launch, algo_launch, launches):
+    """The bound of the dominant decode kernel (both halves use the same kernel
+    on the bundled codes, whose Hx and Hz share a shape)."""
+    from qldpcsim_amd import _lib
+    kernel = names[0]
+    sha = device_code_sha(_lib.LIB_PATH)
+    src, prof = find_profile(kernel, sha)
+    r = {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
+         "kernel": kernel, "kernel_ms_per_launch": t_launch * 1e3, "launches": launches,
+         "units_per_launch": {"half_shots": hs_launch, "half_shot_iterations": it_launch},
+         "hbm": {"algorithmic_bytes_per_launch": algo_launch,
+                 "algorithmic_gbs": algo_launch / t_launch / 1e9,
+                 "algorithmic_model": "SURVEY.md 8d: per executed half-shot iteration w(3E+2n) flooding "
+                                      "(layered: sum_l w(2E_l + sum_{V_l} d_j + 2|V_l|)), w = 4 MS / 8 BP, "
+                                      "+ m+n+4 I/O bytes per half-shot; an HBM-streaming design's bytes, "
+                                      "not what this LDS-resident kernel moves",
+                 "peak_gbs": HBM_PEAK_GBS},
+         "device_code_sha256": sha, "profile": src}
+    if prof is None:
+        r["note"] = ("no counter profile under profiles/ for this kernel build "
+                     "(tools/gpu_profile_roofline.sh regenerates it): bound and frac unmeasured")
+        return r
+    pu = prof["per_half_shot_iteration"]
+    valu = pu["valu_insts"] * it_launch / t_launch / 1e9             # G wave-instructions / s
+    valu_peak = SIMDS * CLOCK_GHZ / VALU_CYCLES
+    lds = pu["lds_cycles"] * it_launch / t_launch / 1e9              # G LDS-array cycles / s (chip)
+    lds_peak = CUS * CLOCK_GHZ
+    traffic = prof["per_half_shot"]["hbm_bytes"] * hs_launch
+    units = {"valu": {"achieved": valu, "peak": valu_peak, "unit": "G VALU wave-instructions/s",
+                      "frac": valu / valu_peak},
+             "lds": {"achieved": lds, "peak": lds_peak, "unit": "G LDS-array cycles/s (all CUs)",
+                     "frac": lds / lds_peak}}
+    bound = max(units, key=lambda k: units[k]["frac"])
+    r.update(bound=bound, achieved=units[bound]["achieved"], peak=units[bound]["peak"],
+             unit=units[bound]["unit"], frac=units[bound]["frac"], traffic=traffic, units=units)
+    r["hbm"].update(achieved_gbs=traffic / t_launch / 1e9, frac=traffic / t_launch / 1e9 / HBM_PEAK_GBS)
+    r["formula"] = ("valu frac = valu_insts/half-shot-iter x iterations/launch x 4 cycles / "
+                    "(1024 SIMDs x 2.4 GHz x launch time); lds frac = lds_cycles/half-shot-iter x "
+                    "iterations/launch / (256 CUs x 2.4 GHz x launch time); per-unit counts from the "
+                    "profile (SQ_INSTS_VALU, SQ_LDS_IDX_ACTIVE; traffic = 2 x FETCH_SIZE + WRITE_SIZE), "
+                    "launch time and iterations from this run")
+    r["profile_clock_ghz"] = prof.get("clock_ghz")
+    return r
+
+
+# ---------------------------------------------------------------------------
+# launcher
+# ---------------------------------------------------------------------------
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawned_rank(rank, world, port, argv):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    run_rank(parse(argv), rank, world, rank)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        world = int(env_world)
+        if args.gpus is not None and args.gpus != world:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world}")
+        run_rank(args, int(os.environ.get("RANK", "0")), world, int(os.environ.get("LOCAL_RANK", "0")))
+        return
+    world = args.gpus or 1
+    if world < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if world == 1:
+        run_rank(args, 0, 1, 0)
+        return
+    # N ranks, no launcher: spawn N fresh processes (this one never touches the
+    # GPU; device_count does not initialise it on this image)
+    import torch
+    import multiprocessing as mp
+    backend = os.environ.get("QLDPC_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if world > ndev and backend == "nccl":
+        raise SystemExit(f"bench.py: --gpus {world} but {ndev} HIP device(s) visible (one GPU per rank; "
+                         "set QLDPC_BENCH_BACKEND=gloo to rehearse with ranks sharing devices)")
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_spawned_rank, args=(r, world, port, argv)) for r in range(world)]
+    for p in procs:
+        p.start()
+    rc = 0
+    for p in procs:
+        p.join()
+        rc = rc or (p.exitcode or 0)
+    if rc:
+        raise SystemExit(f"bench.py: a rank exited with status {rc}")
 
 
 if __name__ == "__main__":

@@ -94,6 +94,13 @@ int qldpc_decode_device(const qldpc_code *code, const qldpc_schedule *sched, int
                         double eps, uint8_t *d_ehat, int32_t *d_iters, double *d_post,
                         int32_t *d_flags, void *stream);
 
+/* Name of the kernel qldpc_decode_device launches for (code, sched, algo),
+ * as rocprofv3 reports it (e.g. "ms_flood_kernel<8, 4>"): lets a benchmark
+ * match its live timings to a committed counter profile. No reference
+ * counterpart (measurement only). */
+int qldpc_decode_kernel_name(const qldpc_code *code, const qldpc_schedule *sched, int algo,
+                             char *buf, int len);
+
 /* Same with host buffers: stages through device memory, synchronous.
  * This is what the single-shot drop-in shims (MS_decoder / BP_decoder) use. */
 int qldpc_decode_host(const qldpc_code *code, const qldpc_schedule *sched, int algo,

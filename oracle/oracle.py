@@ -84,6 +84,12 @@ def decode_batch(algo, H, syn, p, max_iter, layer_ptr=None, layer_rows=None, bet
 # --------------------------------------------------------------------------
 # OSD restatement (decoders.py:299-370, gf2math.py:91-187). Small cases only.
 # --------------------------------------------------------------------------
+def _bits_to_int(v):
+    """uint8/bool vector -> Python int with bit i = v[i]."""
+    v = np.asarray(v, dtype=np.uint8) & 1
+    return int.from_bytes(np.packbits(v, bitorder="little").tobytes(), "little") if v.size else 0
+
+
 def gf2_rank(A):
     """gf2math.rank (gf2math.py:91-135): rank over GF(2), by an XOR basis of
     the bit-packed rows (same value as the reference's row reduction)."""
@@ -91,7 +97,7 @@ def gf2_rank(A):
     basis = {}
     r = 0
     for row in A:
-        v = int("".join("1" if b else "0" for b in row[::-1]), 2) if row.size else 0
+        v = _bits_to_int(row)
         while v:
             h = v.bit_length() - 1
             if h not in basis:
@@ -102,33 +108,49 @@ def gf2_rank(A):
     return r
 
 
+_RANK_CACHE = {}
+
+
+def _rank_of(H):
+    key = (H.shape, np.packbits(np.asarray(H, np.uint8) & 1).tobytes())
+    if key not in _RANK_CACHE:
+        _RANK_CACHE[key] = gf2_rank(H)
+    return _RANK_CACHE[key]
+
+
 def gf2_ref_T(A):
-    """Transform T of gf2math.REF(A, reduced=True) (gf2math.py:139-187)."""
-    B = (np.asarray(A) & 1).astype(np.int8).copy()
-    nR, nC = B.shape
-    T = np.identity(nR, dtype=np.int8)
+    """Transform T of gf2math.REF(A, reduced=True) (gf2math.py:139-187): the
+    same pivot search and row operations, on bit-packed rows [A | T]."""
+    A = (np.asarray(A) & 1).astype(np.uint8)
+    nR, nC = A.shape
+    W = nC + nR
+    bits = np.zeros((nR, W), np.uint8)
+    bits[:, :nC] = A
+    bits[np.arange(nR), nC + np.arange(nR)] = 1
+    words = (W + 63) // 64
+    pk = np.packbits(bits, axis=1, bitorder="little")
+    pk = np.concatenate([pk, np.zeros((nR, words * 8 - pk.shape[1]), np.uint8)], axis=1)
+    R = pk.view(np.uint64).copy()                      # [nR, words]
     x = 0
     for c in range(nC):
-        r = x
-        while r < nR and B[r, c] == 0:
-            r += 1
-        if r == nR:
+        w, b = c >> 6, np.uint64(c & 63)
+        col = ((R[:, w] >> b) & np.uint64(1)).astype(bool)
+        cand = np.flatnonzero(col[x:])
+        if cand.size == 0:
             continue
+        r = x + int(cand[0])
         if r != x:
-            B[[x, r]] = B[[r, x]]
-            T[[x, r]] = T[[r, x]]
-        for s in range(r + 1, nR):
-            if B[s, c]:
-                B[s] ^= B[x]
-                T[s] ^= T[x]
-        for s in range(x):
-            if B[s, c]:
-                B[s] ^= B[x]
-                T[s] ^= T[x]
+            R[[x, r]] = R[[r, x]]
+            col[[x, r]] = col[[r, x]]
+        # rows below the pivot, then rows above it, that hold a 1 in column c
+        others = np.flatnonzero(col)
+        others = others[others != x]
+        R[others] ^= R[x]
         x += 1
         if x >= nR:
             break
-    return T
+    out = np.unpackbits(R.view(np.uint8), axis=1, bitorder="little")[:, nC:nC + nR]
+    return out.astype(np.int8)
 
 
 def osd_dec(H, e_hat, syndrome, post, order=0):
@@ -145,9 +167,9 @@ def osd_dec(H, e_hat, syndrome, post, order=0):
     # gf2math.rank on Hp[:, J] after every append; "rank rose" is restated as
     # "the column is independent of the kept ones" with an incremental XOR
     # basis over bit-packed columns (same J, O(m) per column instead of a full
-    # elimination).
-    cols = [int("".join("1" if b else "0" for b in Hp[::-1, j]), 2) if Hp.shape[0] else 0
-            for j in range(Hp.shape[1])]
+    # elimination). rank(Hp) = rank(H): a column permutation keeps the rank.
+    colbytes = np.packbits(Hp.astype(np.uint8), axis=0, bitorder="little")
+    cols = [int.from_bytes(colbytes[:, j].tobytes(), "little") for j in range(Hp.shape[1])]
     basis = {}
 
     def insert(v):
@@ -159,7 +181,7 @@ def osd_dec(H, e_hat, syndrome, post, order=0):
             v ^= basis[h]
         return False
 
-    max_rank = gf2_rank(Hp)
+    max_rank = _rank_of(H)
     J = [0]
     past = 1 if insert(cols[0]) else 0
     nxt = 1

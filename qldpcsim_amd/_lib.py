@@ -22,7 +22,7 @@ EXPORTS = (
     "qldpc_last_error", "qldpc_version", "qldpc_device_count",
     "qldpc_code_create", "qldpc_code_destroy", "qldpc_code_shape",
     "qldpc_schedule_create", "qldpc_schedule_destroy",
-    "qldpc_decode_device", "qldpc_decode_host",
+    "qldpc_decode_device", "qldpc_decode_host", "qldpc_decode_kernel_name",
     "qldpc_osd_decode", "qldpc_osd_decode_batch", "qldpc_osd_device", "qldpc_cpython_setdiff_first",
     "qldpc_channel_thresholds", "qldpc_channel_sample", "qldpc_count_outcomes",
     "qldpc_timing_enable", "qldpc_timing_reset", "qldpc_timing_read",
@@ -61,6 +61,7 @@ def _load():
         "qldpc_schedule_destroy": ([P], I),
         "qldpc_decode_device": ([P, P, I, P, I64, D, I, D, D, P, P, P, P, P], I),
         "qldpc_decode_host": ([P, P, I, P, I64, D, I, D, D, P, P, P, P], I),
+        "qldpc_decode_kernel_name": ([P, P, I, ctypes.c_char_p, I], I),
         "qldpc_osd_decode": ([P, P, P, I, P, P, P, I], I),
         "qldpc_osd_decode_batch": ([P, I64, P, P, I, P, I], I),
         "qldpc_osd_device": ([P, I64, P, P, I, P, P, P], I),
@@ -172,6 +173,15 @@ def code_for(H, device_index=None):
             c = Code(H)
             _code_cache[key] = c
         return c
+
+
+def kernel_name(H, layer_ptr, layer_rows, algo, device_index=None):
+    """Name of the decode kernel a launch for (H, schedule, algo) uses."""
+    code = code_for(H, device_index)
+    sched = code.schedule(layer_ptr, layer_rows)
+    buf = ctypes.create_string_buffer(128)
+    check(lib.qldpc_decode_kernel_name(code.handle, sched.handle, ALGO[algo], buf, 128))
+    return buf.value.decode()
 
 
 def timing_enable(on=True):

@@ -201,6 +201,7 @@ struct LaunchCfg {
   bool lblob = false;  // uses the layer-ordered blob (ms_layered_kernel)
   bool gtab = false;     // ms_flood_kernel: global tables, LDS = wave state only
   int team = 0;          // bp_team_kernel: waves per half-shot (one workgroup), 0 = wave kernels
+  const char* name = "";  // kernel name as rocprofv3 reports it
   bool ok = false;
 };
 
@@ -480,7 +481,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   int max_waves = QLDPC_MAX_THREADS / 64;
   bool gtab = false;
   if (algo == QLDPC_ALGO_MS && !s->layered && dc > 0 && !s->fblob.empty() && !getenv("QLDPC_NO_REGTAB")) {
-    cfg.kernel = qldpc::select_ms_flood_kernel(dc, (c->m + 63) / 64);
+    cfg.kernel = qldpc::select_ms_flood_kernel(dc, (c->m + 63) / 64, &cfg.name);
     gtab = cfg.kernel != nullptr;
     if (gtab) max_waves = qldpc::ms_flood_max_waves((c->m + 63) / 64);
   }
@@ -491,7 +492,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
     // one (interleaved A/B, DESIGN.md §3.2: wider groups lost on 7-60-row layers)
     int g = s->median_rows <= 2 ? 8 : 1;
     if (const char* ev = getenv("QLDPC_MS_LANES_PER_CHECK")) g = atoi(ev);
-    cfg.kernel = qldpc::select_ms_layered_kernel(dc, g);
+    cfg.kernel = qldpc::select_ms_layered_kernel(dc, g, &cfg.name);
     use_lblob = cfg.kernel != nullptr;
   }
   cfg.lblob = use_lblob;
@@ -504,11 +505,11 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
     team_layout(c, 4, &tb, &o1, &o2, &o3, &o4);
     team = ((int)s->blob.size() + tb > 48 * 1024) ? 8 : 4;
     if (const char* ev = getenv("QLDPC_BP_TEAM_W")) team = atoi(ev);
-    cfg.kernel = qldpc::select_bp_team_kernel(s->layered, dc, team);
+    cfg.kernel = qldpc::select_bp_team_kernel(s->layered, dc, team, &cfg.name);
     if (!cfg.kernel) team = 0;
   }
   cfg.team = team;
-  if (!cfg.kernel) cfg.kernel = qldpc::select_kernel(algo, s->layered, dc);
+  if (!cfg.kernel) cfg.kernel = qldpc::select_kernel(algo, s->layered, dc, &cfg.name);
   int off_c2v, off_synw, off_parw, off_red;
   wave_layout(c, s->layered, algo, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw, use_lblob);
   if (team) team_layout(c, team, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw, &off_red);
@@ -716,6 +717,19 @@ extern "C" int qldpc_decode_device(const qldpc_code* code, const qldpc_schedule*
     std::lock_guard<std::mutex> lk(g_tmu);
     g_events.emplace_back(e0, e1);
   }
+  return QLDPC_OK;
+}
+
+extern "C" int qldpc_decode_kernel_name(const qldpc_code* code, const qldpc_schedule* sched_c, int algo,
+                                        char* buf, int len) {
+  auto* sched = const_cast<qldpc_schedule*>(sched_c);
+  if (!code || !sched || !buf || len <= 0) return fail(QLDPC_EINVAL, "null argument");
+  if (algo != QLDPC_ALGO_MS && algo != QLDPC_ALGO_BP) return fail(QLDPC_EINVAL, "Unrecognized decoder type.");
+  if (code->device < 0 || !sched->d_blob) return fail(QLDPC_EHIP, "no HIP device was visible when the code/schedule was created");
+  LaunchCfg* cfg = nullptr;
+  int rc = launch_config(sched, algo, &cfg);
+  if (rc) return rc;
+  snprintf(buf, (size_t)len, "%s", cfg->name);
   return QLDPC_OK;
 }
 

@@ -39,14 +39,15 @@ struct DecodeArgs {
   uint32_t* queue;            // half-shot work queue (zeroed before the launch), or null = static stride
 };
 
-const void* select_kernel(int algo, bool layered, int dc);
+// `name` (nullable) receives the kernel's name as rocprofv3 reports it
+const void* select_kernel(int algo, bool layered, int dc, const char** name);
 // flooding MS, uniform row degree: global tables (fblob), LDS = wave state only
-const void* select_ms_flood_kernel(int dc, int kc);  // nullptr if no instantiation fits
+const void* select_ms_flood_kernel(int dc, int kc, const char** name);  // nullptr if no instantiation fits
 int ms_flood_max_waves(int kc);                      // waves per workgroup it was compiled for
 // layered MS, uniform row degree 7/8, G = 1/2/4/8 lanes per check (layer-table blob)
-const void* select_ms_layered_kernel(int dc, int g);
+const void* select_ms_layered_kernel(int dc, int g, const char** name);
 // BP, uniform row degree 7/8: one team of W waves per half-shot, edge-parallel check nodes
-const void* select_bp_team_kernel(bool layered, int dc, int w);
+const void* select_bp_team_kernel(bool layered, int dc, int w, const char** name);
 hipError_t launch_decode(const void* kernel, const DecodeArgs& args, int grid, int block,
                          int lds_bytes, hipStream_t stream);
 hipError_t configure_kernel(const void* kernel, int lds_bytes);

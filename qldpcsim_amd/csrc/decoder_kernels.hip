@@ -1584,34 +1584,44 @@ static const void* kernel_ptr() {
 
 int ms_flood_max_waves(int kc) { return (kc >= 8 ? 512 : 256) / 64; }
 
-const void* select_ms_flood_kernel(int dc, int kc) {
+// Kernel names as rocprofv3 reports them (bench.py matches profiles by name).
+#define QLDPC_NAMED(ptr, str) do { if (name) *name = str; return (const void*)ptr; } while (0)
+
+const void* select_ms_flood_kernel(int dc, int kc, const char** name) {
   // instantiated (DC, KC) shapes; the host passes ceil(m/64) checks per lane
-  if (dc == 7 && kc <= 2) return (const void*)&ms_flood_kernel<7, 2>;
-  if (dc == 8 && kc <= 2) return (const void*)&ms_flood_kernel<8, 2>;
-  if (dc == 7 && kc <= 4) return (const void*)&ms_flood_kernel<7, 4>;
-  if (dc == 8 && kc <= 4) return (const void*)&ms_flood_kernel<8, 4>;
-  if (dc == 7 && kc <= 8) return (const void*)&ms_flood_kernel<7, 8>;
-  if (dc == 8 && kc <= 8) return (const void*)&ms_flood_kernel<8, 8>;
+  if (dc == 7 && kc <= 2) QLDPC_NAMED((&ms_flood_kernel<7, 2>), "ms_flood_kernel<7, 2>");
+  if (dc == 8 && kc <= 2) QLDPC_NAMED((&ms_flood_kernel<8, 2>), "ms_flood_kernel<8, 2>");
+  if (dc == 7 && kc <= 4) QLDPC_NAMED((&ms_flood_kernel<7, 4>), "ms_flood_kernel<7, 4>");
+  if (dc == 8 && kc <= 4) QLDPC_NAMED((&ms_flood_kernel<8, 4>), "ms_flood_kernel<8, 4>");
+  if (dc == 7 && kc <= 8) QLDPC_NAMED((&ms_flood_kernel<7, 8>), "ms_flood_kernel<7, 8>");
+  if (dc == 8 && kc <= 8) QLDPC_NAMED((&ms_flood_kernel<8, 8>), "ms_flood_kernel<8, 8>");
   return nullptr;
 }
 
-const void* select_bp_team_kernel(bool layered, int dc, int w) {
-#define QLDPC_BPT(L, D, Wn) if (layered == L && dc == D && w == Wn) return (const void*)&bp_team_kernel<L, D, Wn>;
+const void* select_bp_team_kernel(bool layered, int dc, int w, const char** name) {
+#define QLDPC_BPT(L, D, Wn) \
+  if (layered == L && dc == D && w == Wn) QLDPC_NAMED((&bp_team_kernel<L, D, Wn>), "bp_team_kernel<" #L ", " #D ", " #Wn ">");
   QLDPC_BPT(false, 7, 4) QLDPC_BPT(false, 8, 4) QLDPC_BPT(true, 7, 4) QLDPC_BPT(true, 8, 4)
   QLDPC_BPT(false, 7, 8) QLDPC_BPT(false, 8, 8) QLDPC_BPT(true, 7, 8) QLDPC_BPT(true, 8, 8)
 #undef QLDPC_BPT
   return nullptr;
 }
 
-const void* select_ms_layered_kernel(int dc, int g) {
-#define QLDPC_MSL(D, Gn) if (dc == D && g == Gn) return (const void*)&ms_layered_kernel<D, Gn>;
+const void* select_ms_layered_kernel(int dc, int g, const char** name) {
+#define QLDPC_MSL(D, Gn) if (dc == D && g == Gn) QLDPC_NAMED((&ms_layered_kernel<D, Gn>), "ms_layered_kernel<" #D ", " #Gn ">");
   QLDPC_MSL(7, 1) QLDPC_MSL(8, 1) QLDPC_MSL(7, 2) QLDPC_MSL(8, 2)
   QLDPC_MSL(7, 4) QLDPC_MSL(8, 4) QLDPC_MSL(7, 8) QLDPC_MSL(8, 8)
 #undef QLDPC_MSL
   return nullptr;
 }
 
-const void* select_kernel(int algo, bool layered, int dc) {
+const void* select_kernel(int algo, bool layered, int dc, const char** name) {
+  static const char* names[2][2][3] = {
+      {{"decode_kernel<0, false, 0>", "decode_kernel<0, false, 7>", "decode_kernel<0, false, 8>"},
+       {"decode_kernel<0, true, 0>", "decode_kernel<0, true, 7>", "decode_kernel<0, true, 8>"}},
+      {{"decode_kernel<1, false, 0>", "decode_kernel<1, false, 7>", "decode_kernel<1, false, 8>"},
+       {"decode_kernel<1, true, 0>", "decode_kernel<1, true, 7>", "decode_kernel<1, true, 8>"}}};
+  if (name) *name = names[algo == ALGO_MS ? 0 : 1][layered ? 1 : 0][dc == 7 ? 1 : (dc == 8 ? 2 : 0)];
 #define QLDPC_PICK(ALG)                                                                 \
   switch (dc) {                                                                         \
     case 7: return layered ? kernel_ptr<ALG, true, 7>() : kernel_ptr<ALG, false, 7>();  \

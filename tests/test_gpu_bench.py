@@ -1,7 +1,9 @@
 """bench.py's contract on the GPU: one JSON line with the driver's keys, the
-roofline and CPU-baseline objects, and the multi-rank path (launched as the
-driver does, torch.distributed.run; here 2 ranks share the one GPU over gloo,
-QLDPC_BENCH_BACKEND — on the 8-GPU node it is RCCL, one rank per GPU)."""
+roofline (on-chip bound priced from the committed counter profile) and
+CPU-baseline objects, and the multi-rank paths: spawned by `--gpus N` itself,
+and launched by torch.distributed.run as the driver does. On this one-GPU box
+two ranks share the device over gloo (QLDPC_BENCH_BACKEND); with RCCL,
+`--gpus 2` must refuse to run."""
 import json
 import os
 import subprocess
@@ -23,18 +25,60 @@ def _last_json(out):
     return json.loads(lines[-1])
 
 
+def _bench(*args, env=None, timeout=110):
+    return subprocess.run([sys.executable, "bench.py", *args], cwd=ROOT, capture_output=True, text=True,
+                          timeout=timeout, env=env)
+
+
 def test_bench_single_gpu_line():
-    r = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--batch", "65536",
-                        "--cpu-seconds", "1"], cwd=ROOT, capture_output=True, text=True, timeout=110)
+    r = _bench("--steps", "2", "--warmup", "1", "--batch", "65536", "--cpu-seconds", "1")
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
     assert KEYS <= set(d) and d["n_gpus"] == 1 and d["value"] > 0
-    assert d["roofline"]["bound"] == "hbm" and d["roofline"]["peak"] == 8000.0
-    assert d["cpu_baseline"]["kind"] == "port" and d["cpu_baseline"]["value"] > 0
+    rf = d["roofline"]
+    assert rf["kernel"] == "ms_flood_kernel<8, 4>"
+    assert rf["hbm"]["algorithmic_gbs"] > 0 and rf["hbm"]["peak_gbs"] == 8000.0
+    if rf["profile"] is not None:                  # committed profile of this build
+        assert rf["bound"] in ("valu", "lds") and 0.05 < rf["frac"] <= 1.05
+        assert 0 < rf["hbm"]["frac"] < 1 and rf["traffic"] > 0
+    cb = d["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
+    assert [l["sample"].split("oracle/")[1].split()[0] for l in cb["legs"]] == \
+        ["qldpc_oracle.c,", "numpy_dense.py"]
+    assert cb["reference_context"]["value"] == 2.61
     assert d["config"]["avg_iterations"] == 50.0
 
 
-def test_bench_two_ranks_share_gpu_over_gloo():
+def test_bench_layered_channel_line():
+    r = _bench("--steps", "1", "--warmup", "1", "--batch", "16384", "--cpu-seconds", "0",
+               "--code", "LP118_2", "--schedule", "L", "--p", "0.05")
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert d["roofline"]["kernel"].startswith("ms_layered_kernel<8")
+    assert 1.0 < d["config"]["avg_iterations"] < 10.0
+
+
+def test_bench_spawns_ranks_itself_over_gloo():
+    env = dict(os.environ, QLDPC_BENCH_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    r = _bench("--gpus", "2", "--steps", "1", "--warmup", "1", "--batch", "16384", env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * 16384
+    assert "cpu_baseline" not in d and d["value"] > 0
+
+
+def test_bench_refuses_more_ranks_than_gpus_over_rccl():
+    env = dict(os.environ)
+    env.pop("QLDPC_BENCH_BACKEND", None)
+    env.pop("WORLD_SIZE", None)
+    import torch
+    n = torch.cuda.device_count()
+    r = _bench("--gpus", str(n + 1), "--steps", "1", "--warmup", "0", "--batch", "1024", env=env)
+    assert r.returncode != 0 and "HIP device(s) visible" in r.stderr
+
+
+def test_bench_two_ranks_share_gpu_over_gloo_torchrun():
     env = dict(os.environ, QLDPC_BENCH_BACKEND="gloo")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", "29531", "bench.py", "--gpus", "2",

@@ -1,0 +1,137 @@
+"""Summarise tools/gpu_profile_roofline.sh runs into profiles/<TAG>_roofline.json,
+the per-unit counter profile bench.py prices its roofline with.
+
+usage: python tools/roofline_profile.py TAG [gpurun_out/roof_TAG]
+
+For every profiled config (a subdirectory holding trace/, p1..pN/ rocprofv3
+outputs and the bench --worklog of each run) and every decode kernel in it:
+  per_half_shot_iteration: SQ_INSTS_VALU, SQ_LDS_IDX_ACTIVE (LDS-array cycles),
+      SQ_INSTS_LDS, SQ_INSTS_SALU, SQ_LDS_BANK_CONFLICT, SQ_WAVE_CYCLES (quad),
+      summed over the kernel's dispatches / the executed half-shot iterations
+      the worklog records for those dispatches;
+  per_half_shot: HBM bytes = 2 x FETCH_SIZE (gfx950 half-count correction,
+      MI355X_MICROARCH.md §HBM) + WRITE_SIZE, both KiB -> bytes;
+  busy: valu = SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x cycles), lds =
+      SQ_LDS_IDX_ACTIVE / (256 CUs x cycles), cycles = GRBM_GUI_ACTIVE / 8 XCDs
+      (the profiled run's own clock, for cross-checking bench.py's frac);
+  mean_duration_ns: the kernel-trace --stats average of the trace pass.
+Each counter comes from its own --pmc pass; units from that pass's worklog.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+sys.path.insert(0, ROOT)
+
+
+def kernel_match(row_name, kernel):
+    return ("::" + kernel + "(") in row_name
+
+
+def counters(pass_dir, kernel):
+    """{counter: summed value over the kernel's dispatches}, dispatch count."""
+    per = defaultdict(float)
+    disp = set()
+    for fn in glob.glob(os.path.join(pass_dir, "**", "*counter_collection.csv"), recursive=True):
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                if not kernel_match(row["Kernel_Name"], kernel):
+                    continue
+                per[row["Counter_Name"]] += float(row["Counter_Value"])
+                disp.add(row.get("Dispatch_Id", row.get("Correlation_Id", len(disp))))
+    return dict(per), len(disp)
+
+
+def work(worklog, kernel):
+    with open(worklog) as f:
+        L = [x for x in json.load(f)["launches"] if x["kernel"] == kernel]
+    return len(L), sum(x["half_shots"] for x in L), sum(x["iters"] for x in L)
+
+
+def stats(trace_dir, kernel):
+    for fn in glob.glob(os.path.join(trace_dir, "**", "*kernel_stats.csv"), recursive=True):
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                if kernel_match(row["Name"], kernel):
+                    return float(row["AverageNs"]), int(row["Calls"])
+    return None, 0
+
+
+def summarise_config(d):
+    with open(os.path.join(d, "trace.work.json")) as f:
+        kernels = sorted({x["kernel"] for x in json.load(f)["launches"]})
+    meta = {}
+    if os.path.exists(os.path.join(d, "config.txt")):
+        meta["bench_args"] = open(os.path.join(d, "config.txt")).read().strip()
+    out = []
+    for k in kernels:
+        c = {}
+        ok = True
+        for p in sorted(glob.glob(os.path.join(d, "p*"))):
+            if not os.path.isdir(p):
+                continue
+            vals, nd = counters(p, k)
+            nl, hs, it = work(p + ".work.json", k)
+            if nd != nl:
+                print(f"{p}: {nd} dispatches of {k} but the worklog has {nl}", file=sys.stderr)
+                ok = False
+            for name, v in vals.items():
+                c[name] = (v, hs, it)
+        if not ok or not c:
+            continue
+        per_it = lambda n: c[n][0] / c[n][2]            # noqa: E731
+        per_hs = lambda n: c[n][0] / c[n][1]            # noqa: E731
+        ent = {"kernel": k, **meta,
+               "per_half_shot_iteration": {
+                   "valu_insts": per_it("SQ_INSTS_VALU"),
+                   "lds_cycles": per_it("SQ_LDS_IDX_ACTIVE"),
+                   "lds_insts": per_it("SQ_INSTS_LDS"),
+                   "salu_insts": per_it("SQ_INSTS_SALU"),
+                   "lds_bank_conflict_cycles": per_it("SQ_LDS_BANK_CONFLICT"),
+                   "wave_quad_cycles": per_it("SQ_WAVE_CYCLES")},
+               "per_half_shot": {
+                   "hbm_fetch_bytes": 2 * 1024 * per_hs("FETCH_SIZE"),
+                   "hbm_write_bytes": 1024 * per_hs("WRITE_SIZE")}}
+        ent["per_half_shot"]["hbm_bytes"] = ent["per_half_shot"]["hbm_fetch_bytes"] + \
+            ent["per_half_shot"]["hbm_write_bytes"]
+        # the SQ pass's own dispatches: busy fractions at its measured clock
+        v, hs, it = c["GRBM_GUI_ACTIVE"]
+        cyc = v / 8.0
+        ent["busy"] = {"valu": c["SQ_ACTIVE_INST_VALU"][0] * 4 / 1024 / cyc,
+                       "lds": c["SQ_LDS_IDX_ACTIVE"][0] / 256 / cyc,
+                       "lds_conflict_share": c["SQ_LDS_BANK_CONFLICT"][0] / c["SQ_LDS_IDX_ACTIVE"][0]}
+        ns, calls = stats(os.path.join(d, "trace"), k)
+        ent["mean_duration_ns"] = ns
+        ent["trace_calls"] = calls
+        tnl, ths, tit = work(os.path.join(d, "trace.work.json"), k)
+        if ns:
+            # clock implied by the SQ pass's cycles at the trace pass's duration, per unit of work
+            ent["clock_ghz"] = (cyc / it) / (ns * tnl / tit)
+            ent["trace_units_per_call"] = {"half_shots": ths / tnl, "half_shot_iterations": tit / tnl}
+        out.append(ent)
+    return out
+
+
+def main():
+    tag = sys.argv[1]
+    d = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", f"roof_{tag}")
+    import bench
+    from qldpcsim_amd import _lib
+    doc = {"tag": tag, "device_code_sha256": bench.device_code_sha(_lib.LIB_PATH),
+           "note": "tools/gpu_profile_roofline.sh + tools/roofline_profile.py; one rocprofv3 --pmc pass "
+                   "per counter set; FETCH_SIZE doubled (gfx950), KiB -> bytes",
+           "kernels": []}
+    for cfg in sorted(glob.glob(os.path.join(d, "*", "trace.work.json"))):
+        doc["kernels"] += summarise_config(os.path.dirname(cfg))
+    path = os.path.join(ROOT, "profiles", f"{tag}_roofline.json")
+    with open(path, "w") as f:
+        json.dump(doc, f, indent=1)
+    print(json.dumps(doc, indent=1))
+
+
+if __name__ == "__main__":
+    main()
