@@ -77,6 +77,12 @@ struct qldpc_code {
   std::vector<uint64_t> col_bits;            // [n][mw] column j of H (OSD)
   uint16_t* d_vinv = nullptr;
   int32_t *d_row_ptr = nullptr, *d_col_idx = nullptr;  // CSR for the GPU OSD
+  // layered MS stop-test filters (ms_layered_kernel): 32 fixed random parity
+  // checks of H's rows; wc[c] bit k = row c in check k, avar[v] bit k = parity
+  // of the rows of check k that hold relabeled variable v
+  std::vector<uint32_t> wc, avar;
+  uint32_t filt_all = 0;
+  uint32_t *d_wc = nullptr, *d_rtab = nullptr;  // rtab: [m][8] relabeled variables per row
   // host staging workspace for qldpc_decode_host
   std::mutex ws_mu;
   int64_t ws_cap = 0;
@@ -145,6 +151,17 @@ extern "C" int qldpc_code_create(const uint8_t* h_H, int m, int n, qldpc_code** 
     for (int e = c->row_ptr[r]; e < c->row_ptr[r + 1]; ++e)
       c->col_bits[(size_t)c->col_idx[e] * c->mw + (r >> 6)] |= 1ull << (r & 63);
   c->rank = gf2_rank_cols(c->col_bits, n, c->mw);
+  c->wc.resize(m);
+  for (int r = 0; r < m; ++r) {
+    uint64_t z = 0x9E3779B97F4A7C15ull * (uint64_t)(r + 1) + 0xD1B54A32D192ED03ull;   // splitmix64
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    c->wc[r] = (uint32_t)((z ^ (z >> 31)) >> 16);
+  }
+  c->avar.assign(n, 0);
+  for (int r = 0; r < m; ++r)
+    for (int e = c->row_ptr[r]; e < c->row_ptr[r + 1]; ++e) c->avar[c->vinv[c->col_idx[e]]] ^= c->wc[r];
+  for (int v = 0; v < n; ++v) c->filt_all ^= c->avar[v];
   if (n > 0 && c->device >= 0) {
     std::vector<uint16_t> v16(c->vinv.begin(), c->vinv.end());
     hipError_t e1 = hipMalloc(&c->d_vinv, sizeof(uint16_t) * n);
@@ -153,6 +170,16 @@ extern "C" int qldpc_code_create(const uint8_t* h_H, int m, int n, qldpc_code** 
     if (e1 == hipSuccess) e1 = hipMemcpy(c->d_row_ptr, c->row_ptr.data(), sizeof(int32_t) * (m + 1), hipMemcpyHostToDevice);
     if (e1 == hipSuccess) e1 = hipMalloc(&c->d_col_idx, sizeof(int32_t) * std::max(1, c->E));
     if (e1 == hipSuccess && c->E) e1 = hipMemcpy(c->d_col_idx, c->col_idx.data(), sizeof(int32_t) * c->E, hipMemcpyHostToDevice);
+    if (e1 == hipSuccess && m > 0) {
+      std::vector<uint32_t> rtab((size_t)8 * m, 0);
+      for (int r = 0; r < m; ++r)
+        for (int e = c->row_ptr[r], k = 0; e < c->row_ptr[r + 1] && k < 8; ++e, ++k)
+          rtab[(size_t)8 * r + k] = (uint32_t)c->vinv[c->col_idx[e]];
+      e1 = hipMalloc(&c->d_wc, sizeof(uint32_t) * m);
+      if (e1 == hipSuccess) e1 = hipMemcpy(c->d_wc, c->wc.data(), sizeof(uint32_t) * m, hipMemcpyHostToDevice);
+      if (e1 == hipSuccess) e1 = hipMalloc(&c->d_rtab, sizeof(uint32_t) * 8 * m);
+      if (e1 == hipSuccess) e1 = hipMemcpy(c->d_rtab, rtab.data(), sizeof(uint32_t) * 8 * m, hipMemcpyHostToDevice);
+    }
     if (e1 != hipSuccess) {
       delete c;
       return fail(QLDPC_EHIP, "uploading the graph failed: %s", hipGetErrorString(e1));
@@ -179,6 +206,8 @@ extern "C" int qldpc_code_destroy(qldpc_code* code) {
   (void)hipFree(code->d_vinv);
   (void)hipFree(code->d_row_ptr);
   (void)hipFree(code->d_col_idx);
+  (void)hipFree(code->d_wc);
+  (void)hipFree(code->d_rtab);
   ws_free(code);
   delete code;
   return QLDPC_OK;
@@ -362,7 +391,7 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
       s->l_off_adj_ptr = put(s->lblob, adj_ptr);
       s->l_off_adj_info = put(s->lblob, adj_info);
       s->l_off_adj_dmax = put(s->lblob, adj_dmax);
-      s->l_off_vn_chk = put(s->lblob, vn_chk);
+      s->l_off_vn_chk = put(s->lblob, code->avar);   // filter word per relabeled variable
       s->lblob.resize(align16((int)s->lblob.size() + 1));
     }
   }
@@ -447,7 +476,7 @@ static void wave_layout(const qldpc_code* c, bool layered, int algo, int* bytes,
   *off_synw = off;
   if (layered) off = align16(off + 4 * words);
   *off_parw = off;
-  if (layered) off = align16(off + 4 * words);
+  if (layered && !colsum_f32) off = align16(off + 4 * words);  // ms_layered_kernel: filters, no parity words
   *bytes = std::max(off, 16);
 }
 
@@ -687,6 +716,17 @@ extern "C" int qldpc_decode_device(const qldpc_code* code, const qldpc_schedule*
   a.beta = beta;
   a.eps = eps;
   a.max_iter = max_iter;
+  a.wc = code->d_wc;
+  a.rtab = code->d_rtab;
+  a.filt_all = code->filt_all;
+  {
+    // (L + (double)S < 0) == (S < hd_thresh) for every float S: the float at
+    // or below -L, nudged up one step when -L is not a float
+    const double t = -a.L;
+    float f = (float)t;
+    if ((double)f > t) f = std::nextafter(f, -INFINITY);
+    a.hd_thresh = ((double)f == t) ? f : std::nextafter(f, INFINITY);
+  }
 
   a.queue = nullptr;
   if (!getenv("QLDPC_STATIC_SCHED")) {

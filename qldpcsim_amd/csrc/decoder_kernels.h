@@ -37,6 +37,12 @@ struct DecodeArgs {
   double beta, eps;
   int max_iter;
   uint32_t* queue;            // half-shot work queue (zeroed before the launch), or null = static stride
+  // ms_layered_kernel's stop-test filters: 32 random parity
+  // checks w_k of H's rows; wc[c] = bit k set if w_k holds row c
+  const uint32_t* wc;         // [m]   global
+  const uint32_t* rtab;       // [m][8] relabeled variables of each row (global; exact stop test)
+  uint32_t filt_all;          // XOR of every variable's filter word (all hard decisions 1)
+  float hd_thresh;            // hard decision of a column sum S: (L + (f64)S < 0) == (S < hd_thresh)
 };
 
 // `name` (nullable) receives the kernel's name as rocprofv3 reports it

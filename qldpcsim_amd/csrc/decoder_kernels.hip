@@ -1142,18 +1142,30 @@ __device__ __forceinline__ void cn_ms_split(const DecodeArgs& a, const uint32_t*
 // (variable, csc start | degree) so every phase is one dependent LDS hop
 // shorter than decode_kernel<MS, true, DC>.
 // ---------------------------------------------------------------------------
+// XOR of a 32-bit value over the 64 lanes (all lanes active): DPP within each
+// row of 16 lanes, then the four row results.
+constexpr int kDppRowMirror = 0x140;   // row_mirror: lane i <-> 15-i within 16
+__device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
+  x ^= dpp_u32<kDppQuadXor1>(x);
+  x ^= dpp_u32<kDppQuadXor2>(x);
+  x ^= dpp_u32<kDppHalfMirror>(x);
+  x ^= dpp_u32<kDppRowMirror>(x);
+  return (uint32_t)(__builtin_amdgcn_readlane((int)x, 0) ^ __builtin_amdgcn_readlane((int)x, 16) ^
+                    __builtin_amdgcn_readlane((int)x, 32) ^ __builtin_amdgcn_readlane((int)x, 48));
+}
+
 // Variable-node pass of one layer (decoders.py:172-174 over the layer's
 // adjacent variables) for a wave-uniform degree bound K: two 64-variable
 // chunks per trip with every LDS read of both issued before the sums (the
-// chunks' variables are distinct, so their post writes never alias the other
-// chunk's reads), then the parity toggles of flipped hard decisions. Measured
-// (interleaved A/B): LP118_2 MS-L -16..-18 %, LP118_0 -9 %; toggles with the
-// check ids hoisted and one predicated atomic per term were slower than this
-// per-lane loop (only flipped lanes iterate, over their own degree).
+// chunks' variables are distinct, so their colS writes never alias the other
+// chunk's reads). Hard decisions are compared in the float32 domain
+// (S < hd_thresh is exactly L + (f64)S < 0). Each flipped hard decision
+// contributes its variable's filter word (stop test, ms_layered_kernel); the
+// lane-local XOR is returned.
 template <int K>
-__device__ __forceinline__ void vn_layer(const uint32_t* adj_info, const uint16_t* vn_chk, float* colS,
-                                         const float* c2v, uint32_t* parw, int v0, int v1, int lane,
-                                         double L) {
+__device__ __forceinline__ uint32_t vn_layer(const uint32_t* adj_info, const uint32_t* avar, float* colS,
+                                             const float* c2v, int v0, int v1, int lane, float thr) {
+  uint32_t acc = 0;
   for (int qb = v0; qb < v1; qb += 128) {
     uint32_t info[2];
     bool in[2];
@@ -1163,38 +1175,57 @@ __device__ __forceinline__ void vn_layer(const uint32_t* adj_info, const uint16_
       in[h] = q < v1;
       info[h] = adj_info[in[h] ? q : v0];
     }
-    double old[2];
+    float old[2];
+    uint32_t av[2];
     float x[2][K];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      old[h] = L + (double)colS[info[h] >> 21];          // post before this layer
+      old[h] = colS[info[h] >> 21];                         // column sum before this layer
+      av[h] = avar[info[h] >> 21];
       const float* c = c2v + (info[h] & 0xffffu);
 #pragma unroll
       for (int t = 0; t < K; ++t) x[h][t] = c[t];          // c2v padded by 8 floats
     }
-    bool flip[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int d = (int)((info[h] >> 16) & 31u);
-      float s = 0.0f;                                     // sequential, ascending check (:172)
+      float s = 0.0f;                                       // sequential, ascending check (:172)
 #pragma unroll
       for (int t = 0; t < K; ++t) s += (t < d) ? x[h][t] : 0.0f;
-      const double nw = L + (double)s;                    // (:173)
       if (in[h]) colS[info[h] >> 21] = s;
-      flip[h] = in[h] && ((old[h] < 0.0) != (nw < 0.0));  // hard decision flipped (:174)
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (flip[h]) {
-        for (int p = (int)(info[h] & 0xffffu), pe = p + (int)((info[h] >> 16) & 31u); p < pe; ++p) {
-          const int c = vn_chk[p];
-          atomicXor(&parw[c >> 5], 1u << (c & 31));
-        }
-      }
+      const bool flip = in[h] && ((old[h] < thr) != (s < thr));   // hard decision flipped (:173-174)
+      acc ^= flip ? av[h] : 0u;
     }
   }
+  return acc;
 }
 
+// Exact stop test (decoders.py:175-176): every row's parity of the current
+// hard decisions against its syndrome bit. Runs only when the filters pass.
+template <int DC>
+__device__ __forceinline__ bool layered_full_check(const DecodeArgs& a, const float* colS, const uint32_t* synw,
+                                                   int lane, float thr) {
+  uint32_t un = 0;
+  for (int c = lane; c < a.m; c += 64) {
+    const uint4 t0 = *(const uint4*)(a.rtab + 8 * (size_t)c);
+    const uint4 t1 = *(const uint4*)(a.rtab + 8 * (size_t)c + 4);
+    const uint32_t t[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+    uint32_t par = 0;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) par ^= (uint32_t)(colS[t[k]] < thr);
+    un |= par ^ ((synw[c >> 5] >> (c & 31)) & 1u);
+  }
+  return ballot(un != 0) == 0;
+}
+
+// Stop test without per-check parity state: 32 fixed random parity checks
+// w_k of H's rows. If H e = s then w_k H e = w_k s for every k, so the layer
+// can only have converged when the 32 filter parities of the hard decisions
+// (F, updated by the flipped variables' words a_j = bit k of w_k H) equal those
+// of the syndrome (B); then the exact row-by-row test decides. A state with
+// H e != s passes all 32 filters with probability 2^-32, so the exact test
+// runs about once per decode, and the per-flip parity toggles (LDS atomics,
+// one per edge of every flipped variable) are gone.
 template <int DC, int G>
 __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -1211,7 +1242,7 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
   const uint16_t* adj_ptr = (const uint16_t*)(lds + a.off_adj_ptr);  // [L+1]
   const uint32_t* adj_info = (const uint32_t*)(lds + a.off_row_ptr); // [A] var<<21 | deg<<16 | csc start
   const uint8_t* adj_dmax = (const uint8_t*)(lds + a.off_chunk_dmax);// [L] max degree per layer
-  const uint16_t* vn_chk = (const uint16_t*)(lds + a.off_vn_chk);
+  const uint32_t* avar = (const uint32_t*)(lds + a.off_vn_chk);      // [n] filter word per variable
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int waves = blockDim.x >> 6;
@@ -1222,10 +1253,9 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
   unsigned char* c2v_b = ws + a.off_c2v;
   float* c2v = (float*)c2v_b;
   uint32_t* synw = (uint32_t*)(ws + a.off_synw);
-  uint32_t* parw = (uint32_t*)(ws + a.off_parw);
   const uint32_t post_b = lds_addr(colS), c2v_a = lds_addr(c2v_b);
   const int m = a.m, n = a.n;
-  const int nwords = (m + 31) >> 5;
+  const float thr = a.hd_thresh;
   VinvRegs<16> vr;                                             // n <= 1024 in registers
   vr.load(a.vinv, n, lane);
 
@@ -1240,9 +1270,13 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
     load_syndrome_bits<8>(syn, m, synw, lane);
     for (int j = lane; j < n; j += 64) colS[j] = 0.0f;          // post = L, c2v = 0 (:148-150)
     for (int p = lane; p < a.E; p += 64) c2v[p] = 0.0f;
-    for (int c0 = 0; c0 < m; c0 += 64)
-      store_bits64(parw, c0, (c0 + lane < m) && (L < 0.0) && (DC & 1), lane);
     wave_sync();
+    // filter parities of the syndrome (B) and of the hard decisions (F: all
+    // variables start at post = L, so all ones iff L < 0)
+    uint32_t bl = 0;
+    for (int c = lane; c < m; c += 64) bl ^= ((synw[c >> 5] >> (c & 31)) & 1u) ? a.wc[c] : 0u;
+    const uint32_t B = wave_xor(bl);
+    uint32_t F = (L < 0.0) ? a.filt_all : 0u;
     bool first = true;
     for (int it = 0; it < a.max_iter && !conv; ++it) {
       for (int l = 0; l < a.n_layers; ++l) {
@@ -1286,31 +1320,26 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
         // other columns are unchanged, so this equals the full recompute)
         const int v0 = adj_ptr[l], v1 = adj_ptr[l + 1];
         const int dmax = __builtin_amdgcn_readfirstlane((int)adj_dmax[l]);
+        uint32_t acc = 0;
         switch (dmax) {
-          case 3: vn_layer<3>(adj_info, vn_chk, colS, c2v, parw, v0, v1, lane, L); break;
-          case 4: vn_layer<4>(adj_info, vn_chk, colS, c2v, parw, v0, v1, lane, L); break;
-          case 5: vn_layer<5>(adj_info, vn_chk, colS, c2v, parw, v0, v1, lane, L); break;
-          case 6: vn_layer<6>(adj_info, vn_chk, colS, c2v, parw, v0, v1, lane, L); break;
+          case 3: acc = vn_layer<3>(adj_info, avar, colS, c2v, v0, v1, lane, thr); break;
+          case 4: acc = vn_layer<4>(adj_info, avar, colS, c2v, v0, v1, lane, thr); break;
+          case 5: acc = vn_layer<5>(adj_info, avar, colS, c2v, v0, v1, lane, thr); break;
+          case 6: acc = vn_layer<6>(adj_info, avar, colS, c2v, v0, v1, lane, thr); break;
           default:
             for (int q = v0 + lane; q < v1; q += 64) {
               const uint32_t info = adj_info[q];
               const int j = (int)(info >> 21), d = (int)((info >> 16) & 31u);
-              const double old = L + (double)colS[j];
+              const float old = colS[j];
               const float s = ms_colsum_sw(c2v + (info & 0xffffu), d, dmax);
-              const double nw = L + (double)s;
               colS[j] = s;
-              if ((old < 0.0) != (nw < 0.0)) {                   // hard decision flipped
-                for (int p = (int)(info & 0xffffu), pe = p + d; p < pe; ++p) {
-                  const int c = vn_chk[p];
-                  atomicXor(&parw[c >> 5], 1u << (c & 31));
-                }
-              }
+              if ((old < thr) != (s < thr)) acc ^= avar[j];       // hard decision flipped
             }
         }
+        F ^= wave_xor(acc);
         wave_sync();
-        uint32_t un = 0;                                         // stop test (:175-176)
-        for (int w = lane; w < nwords; w += 64) un |= parw[w] ^ synw[w];
-        if (ballot(un != 0) == 0) {
+        // stop test (:175-176): filters first, the exact test only if they pass
+        if (F == B && layered_full_check<DC>(a, colS, synw, lane, thr)) {
           iters = it + 1;
           conv = true;
           break;
