@@ -230,6 +230,8 @@ struct LaunchCfg {
   bool lblob = false;  // uses the layer-ordered blob (ms_layered_kernel)
   bool gtab = false;     // ms_flood_kernel: global tables, LDS = wave state only
   int team = 0;          // bp_team_kernel: waves per half-shot (one workgroup), 0 = wave kernels
+  int nh = 1;            // ms_layered_grp_kernel: half-shots per wave
+  int slice = 0;         // ms_layered_grp_kernel: bytes of one half-shot's LDS slice
   const char* name = "";  // kernel name as rocprofv3 reports it
   bool ok = false;
 };
@@ -239,6 +241,7 @@ struct qldpc_schedule {
   bool layered = false;
   int n_layers = 0;
   int median_rows = 0;        // rows of the median layer (layered MS lanes-per-check choice)
+  int layer_g = 0;            // lanes per check shared by every layer, 0 = chosen per layer
   std::vector<uint8_t> blob;  // LDS image of the graph tables
   // layered MS, uniform degree: layer-ordered tables (ms_layered_kernel)
   std::vector<uint8_t> lblob;
@@ -383,8 +386,18 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
         for (int q = adj_ptr[l]; q < adj_ptr[l + 1]; ++q) {
           const int v = adj_vars[q], d = code->csc_ptr[v + 1] - code->csc_ptr[v];
           adj_info[q] = ((uint32_t)v << 21) | ((uint32_t)d << 16) | (uint32_t)code->csc_ptr[v];
-          adj_dmax[l] = (uint8_t)std::min(255, std::max<int>(adj_dmax[l], d));
+          adj_dmax[l] = (uint8_t)std::max<int>(adj_dmax[l], d);   // d <= 31 here
         }
+      // bits 5-6: log2 of the layer's lanes per check (ms_layered_kernel<DC, 0>):
+      // one lane per check for long layers, a lane group when the layer leaves
+      // most of the wave idle (rows <= 8: 8 lanes, <= 16: 4)
+      s->layer_g = -2;
+      for (int l = 0; l < n_layers; ++l) {
+        const int rows = lay_ptr[l + 1] - lay_ptr[l];
+        const int gl = rows <= 8 ? 3 : (rows <= 16 ? 2 : 0);
+        adj_dmax[l] = (uint8_t)(adj_dmax[l] | (gl << 5));
+        s->layer_g = (s->layer_g == -2 || s->layer_g == (1 << gl)) ? (1 << gl) : 0;
+      }
       s->l_off_ltab = put(s->lblob, ltab);
       s->l_off_lrow = put(s->lblob, lay_rows);
       s->l_off_lay_ptr = put(s->lblob, lay_ptr);
@@ -480,6 +493,16 @@ static void wave_layout(const qldpc_code* c, bool layered, int algo, int* bytes,
   *bytes = std::max(off, 16);
 }
 
+// ms_layered_grp_kernel's per-half-shot slice: colS f32[n] | c2v f32[E + 8] | syndrome u8[m]
+static void grp_layout(const qldpc_code* c, int* bytes, int* off_c2v, int* off_synb) {
+  int off = align16(4 * c->n);
+  *off_c2v = off;
+  off = align16(off + 4 * (c->E + 8));
+  *off_synb = off;
+  off = align16(off + c->m);
+  *bytes = off;
+}
+
 // bp_team_kernel's slice: post f64[n] | c2v f64[E + 8] | syn words | parity
 // words | reduction slots ([2][W] any-flags, [2][2] tickets)
 static void team_layout(const qldpc_code* c, int w, int* bytes, int* off_c2v, int* off_synw,
@@ -519,9 +542,22 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
       !getenv("QLDPC_NO_LAYERED_FAST")) {
     // lanes per check: 8 for one- or two-row layers (serial schedules), else
     // one (interleaved A/B, DESIGN.md §3.2: wider groups lost on 7-60-row layers)
-    int g = s->median_rows <= 2 ? 8 : 1;
+    // lanes per check: one template width when every layer wants the same,
+    // else chosen per layer (the runtime switch costs ~5 % where it is not needed)
+    int g = s->layer_g > 0 ? s->layer_g : 0;
     if (const char* ev = getenv("QLDPC_MS_LANES_PER_CHECK")) g = atoi(ev);
-    cfg.kernel = qldpc::select_ms_layered_kernel(dc, g, &cfg.name);
+    // ms_layered_grp_kernel (several half-shots per wave) only on request:
+    // at a fixed LDS budget it halves the waves per CU, and the layered
+    // kernels are latency-bound (interleaved A/B: LP118_2 MS-L 35 -> 75 ms)
+    int nh = 1;
+    if (const char* ev = getenv("QLDPC_MS_GROUPS")) nh = atoi(ev);
+    if (nh > 1 || getenv("QLDPC_MS_GRP_G")) {
+      int gg = (s->median_rows * 2 <= 64 / nh) ? 2 : 1;
+      if (const char* ev = getenv("QLDPC_MS_GRP_G")) gg = atoi(ev);
+      cfg.kernel = qldpc::select_ms_layered_grp_kernel(dc, nh, gg, &cfg.name);
+      if (cfg.kernel) cfg.nh = nh;
+    }
+    if (!cfg.kernel) cfg.kernel = qldpc::select_ms_layered_kernel(dc, g, &cfg.name);
     use_lblob = cfg.kernel != nullptr;
   }
   cfg.lblob = use_lblob;
@@ -542,6 +578,10 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   int off_c2v, off_synw, off_parw, off_red;
   wave_layout(c, s->layered, algo, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw, use_lblob);
   if (team) team_layout(c, team, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw, &off_red);
+  if (cfg.nh > 1 || (use_lblob && cfg.name && strstr(cfg.name, "grp"))) {
+    grp_layout(c, &cfg.slice, &off_c2v, &off_synw);
+    cfg.wave_bytes = cfg.nh * cfg.slice;
+  }
   int max_lds = 0, dev = 0;
   HIP_TRY(hipGetDevice(&dev));
   HIP_TRY(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
@@ -694,6 +734,7 @@ extern "C" int qldpc_decode_device(const qldpc_code* code, const qldpc_schedule*
     a.off_vn_chk = sched->l_off_vn_chk;
   }
   if (cfg->team) team_layout(code, cfg->team, &a.wave_bytes, &a.off_c2v, &a.off_synw, &a.off_parw, &a.off_red);
+  if (cfg->slice) grp_layout(code, &a.wave_bytes, &a.off_c2v, &a.off_synw);   // per half-shot slice
   if (cfg->gtab) {  // global tables; the LDS holds wave state only
     a.blob = sched->d_fblob;
     a.blob_bytes = 0;
@@ -734,7 +775,8 @@ extern "C" int qldpc_decode_device(const qldpc_code* code, const qldpc_schedule*
   }
   int cus = 0;
   HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  const int64_t need = cfg->team ? batch : (batch + cfg->waves - 1) / cfg->waves;
+  const int64_t per_block = cfg->team ? 1 : (int64_t)cfg->waves * cfg->nh;
+  const int64_t need = (batch + per_block - 1) / per_block;
   const int64_t resident = (int64_t)cfg->blocks_per_cu * cus;
   const int grid = (int)std::max<int64_t>(1, std::min(need, resident));
   hipStream_t st = (hipStream_t)stream;

@@ -38,6 +38,9 @@
 #ifndef QLDPC_ABLATE
 #define QLDPC_ABLATE 0  // timing-only builds: 1 = skip VN, 2 = skip CN (flooding)
 #endif
+#ifndef QLDPC_ABLATE_L
+#define QLDPC_ABLATE_L 0  // timing-only builds of ms_layered_kernel: bit 0 skips CN, bit 1 VN, bit 2 the filter
+#endif
 
 namespace qldpc {
 
@@ -1218,6 +1221,50 @@ __device__ __forceinline__ bool layered_full_check(const DecodeArgs& a, const fl
   return ballot(un != 0) == 0;
 }
 
+// Check nodes of one layer (rows q0..q1 of the layer-ordered table) with GG
+// lanes per check: GG = 1 walks a row's DC edges in one lane (cn_ms_compute),
+// GG > 1 splits them over a lane group (cn_ms_split). All rows read the same
+// snapshot of the column sums (Jacobi within the layer, decoders.py:155-169).
+template <int DC, int GG>
+__device__ __forceinline__ void cn_layer(const DecodeArgs& a, const uint32_t* ltab, const uint16_t* lrow,
+                                         const uint32_t* synw, int q0, int q1, int lane, bool first,
+                                         const float* colS, unsigned char* c2v_b, uint32_t post_b,
+                                         uint32_t c2v_a, int& fl) {
+  if constexpr (GG == 1) {
+    for (int q = q0 + lane; q < q1; q += 64) {
+      uint32_t t[1][8];
+      load_row8(ltab + q * 8, t[0]);
+      const int c = lrow[q];
+      const uint32_t sb[1] = {(synw[c >> 5] >> (c & 31)) & 1u};
+      const bool live[1] = {true};
+      if (first) {
+        (void)cn_ms_uniform<DC, true, 1>(a, t, sb, live, (const unsigned char*)colS, c2v_b, fl);
+      } else {
+        CnLoad<DC> Ld;
+        uint32_t ca[8];
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+          ca[k] = c2v_a + (t[0][k] >> 16);
+          Ld.pj[k] = a.L + (double)*QLDPC_LDS(const float, post_b + (t[0][k] & 0xffffu));   // (:173)
+          Ld.cv[k] = *QLDPC_LDS(const float, ca[k]);
+        }
+        (void)cn_ms_compute<DC>(a, Ld, ca, sb[0], 1u, fl);
+      }
+    }
+  } else {
+    // 64 / GG checks per pass; every lane takes part in the group swaps, so
+    // the loop runs wave-uniformly
+    for (int qb = q0; qb < q1; qb += 64 / GG) {
+      const int q = qb + lane / GG;
+      const bool live = q < q1;
+      const int qs = live ? q : q0;
+      const int c = lrow[qs];
+      const uint32_t sb = (synw[c >> 5] >> (c & 31)) & 1u;
+      cn_ms_split<DC, GG>(a, ltab + qs * 8, lane & (GG - 1), live, sb, first, post_b, c2v_a, fl);
+    }
+  }
+}
+
 // Stop test without per-check parity state: 32 fixed random parity checks
 // w_k of H's rows. If H e = s then w_k H e = w_k s for every k, so the layer
 // can only have converged when the 32 filter parities of the hard decisions
@@ -1281,37 +1328,16 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
     for (int it = 0; it < a.max_iter && !conv; ++it) {
       for (int l = 0; l < a.n_layers; ++l) {
         const int q0 = lay_ptr[l], q1 = lay_ptr[l + 1];
-        if constexpr (G == 1) {
-          for (int q = q0 + lane; q < q1; q += 64) {
-            uint32_t t[1][8];
-            load_row8(ltab + q * 8, t[0]);
-            const int c = lrow[q];
-            const uint32_t sb[1] = {(synw[c >> 5] >> (c & 31)) & 1u};
-            const bool live[1] = {true};
-            if (first) {
-              (void)cn_ms_uniform<DC, true, 1>(a, t, sb, live, (const unsigned char*)colS, c2v_b, fl);
-            } else {
-              CnLoad<DC> Ld;
-              uint32_t ca[8];
-#pragma unroll
-              for (int k = 0; k < DC; ++k) {
-                ca[k] = c2v_a + (t[0][k] >> 16);
-                Ld.pj[k] = a.L + (double)*QLDPC_LDS(const float, post_b + (t[0][k] & 0xffffu));   // (:173)
-                Ld.cv[k] = *QLDPC_LDS(const float, ca[k]);
-              }
-              (void)cn_ms_compute<DC>(a, Ld, ca, sb[0], 1u, fl);
-            }
-          }
+        if constexpr ((QLDPC_ABLATE_L & 1) != 0) {
+        } else if constexpr (G != 0) {
+          cn_layer<DC, G>(a, ltab, lrow, synw, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl);
         } else {
-          // G lanes per check, 64 / G checks per pass; every lane takes part
-          // in the group swaps, so the loop runs wave-uniformly
-          for (int qb = q0; qb < q1; qb += 64 / G) {
-            const int q = qb + lane / G;
-            const bool live = q < q1;
-            const int qs = live ? q : q0;
-            const int c = lrow[qs];
-            const uint32_t sb = (synw[c >> 5] >> (c & 31)) & 1u;
-            cn_ms_split<DC, G>(a, ltab + qs * 8, lane & (G - 1), live, sb, first, post_b, c2v_a, fl);
+          // lanes per check chosen per layer by the host (bits 5-6 of adj_dmax)
+          switch (__builtin_amdgcn_readfirstlane((int)adj_dmax[l]) >> 5) {
+            case 0: cn_layer<DC, 1>(a, ltab, lrow, synw, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl); break;
+            case 1: cn_layer<DC, 2>(a, ltab, lrow, synw, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl); break;
+            case 2: cn_layer<DC, 4>(a, ltab, lrow, synw, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl); break;
+            default: cn_layer<DC, 8>(a, ltab, lrow, synw, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl); break;
           }
         }
         first = false;
@@ -1319,9 +1345,10 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
         // VN over the layer's adjacent variables (decoders.py:172-174: the
         // other columns are unchanged, so this equals the full recompute)
         const int v0 = adj_ptr[l], v1 = adj_ptr[l + 1];
-        const int dmax = __builtin_amdgcn_readfirstlane((int)adj_dmax[l]);
+        const int dmax = __builtin_amdgcn_readfirstlane((int)adj_dmax[l]) & 31;
         uint32_t acc = 0;
-        switch (dmax) {
+        switch ((QLDPC_ABLATE_L & 2) ? -1 : dmax) {
+          case -1: break;
           case 3: acc = vn_layer<3>(adj_info, avar, colS, c2v, v0, v1, lane, thr); break;
           case 4: acc = vn_layer<4>(adj_info, avar, colS, c2v, v0, v1, lane, thr); break;
           case 5: acc = vn_layer<5>(adj_info, avar, colS, c2v, v0, v1, lane, thr); break;
@@ -1336,7 +1363,7 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
               if ((old < thr) != (s < thr)) acc ^= avar[j];       // hard decision flipped
             }
         }
-        F ^= wave_xor(acc);
+        if constexpr ((QLDPC_ABLATE_L & 4) == 0) F ^= wave_xor(acc);
         wave_sync();
         // stop test (:175-176): filters first, the exact test only if they pass
         if (F == B && layered_full_check<DC>(a, colS, synw, lane, thr)) {
@@ -1369,6 +1396,287 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
       if (a.flags) a.flags[hs] = (int32_t)((b1 ? FLAG_MIN_ZERO : 0) | (conv ? FLAG_CONVERGED : 0));
     }
     wave_sync();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Layered / serial min-sum with NH half-shots per wavefront (LPH = 64 / NH
+// lanes each). Layers are short (LP118_0: 16 / 32 rows, 128-208 adjacent
+// variables), so with one half-shot per wave most lanes idle in the check
+// node and every per-layer fixed cost (stop test, loop control, barriers) is
+// paid per half-shot. Here each lane group runs its own half-shot, iteration
+// and layer: a group that converges (or reaches max_iter) writes its outputs
+// and starts its next half-shot while the others carry on, so early-stopping
+// decodes waste no lanes. Same arithmetic as ms_layered_kernel, bit for bit:
+// CN over the layer's rows with G lanes per check (cn_ms_split), VN over the
+// layer's adjacent variables, filtered stop test with the exact check behind
+// it. Loops run to the largest bound among the groups, with per-lane masks.
+// ---------------------------------------------------------------------------
+template <int LPH>
+__device__ __forceinline__ uint32_t group_xor(uint32_t x, int grp) {
+  x ^= dpp_u32<kDppQuadXor1>(x);
+  x ^= dpp_u32<kDppQuadXor2>(x);
+  x ^= dpp_u32<kDppHalfMirror>(x);
+  x ^= dpp_u32<kDppRowMirror>(x);
+  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 0), r1 = (uint32_t)__builtin_amdgcn_readlane((int)x, 16);
+  const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)x, 32), r3 = (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
+  if constexpr (LPH == 16) {
+    return grp == 0 ? r0 : grp == 1 ? r1 : grp == 2 ? r2 : r3;
+  } else if constexpr (LPH == 32) {
+    return grp == 0 ? (r0 ^ r1) : (r2 ^ r3);
+  } else {
+    return r0 ^ r1 ^ r2 ^ r3;
+  }
+}
+
+// wave-wide maximum of a group-uniform non-negative value
+template <int LPH>
+__device__ __forceinline__ int groups_max(int x) {
+  int r = __builtin_amdgcn_readlane(x, 0);
+#pragma unroll
+  for (int g = 1; g < 64 / LPH; ++g) r = max(r, __builtin_amdgcn_readlane(x, g * LPH));
+  return r;
+}
+
+template <int LPH>
+__device__ __forceinline__ uint64_t group_mask(int grp) {
+  return LPH == 64 ? ~0ull : (((1ull << (LPH & 63)) - 1ull) << (LPH * grp));
+}
+
+// Per-group half-shot queue (HalfShotQueue's guided chunks, claimed by the
+// group's first lane and broadcast to the group).
+struct GroupQueue {
+  long long hs, end, stride, batch;
+  uint32_t* q;
+  uint32_t tk, tlen, seen;
+  __device__ __forceinline__ GroupQueue(const DecodeArgs& a, long long slot, long long stride_)
+      : hs(slot), end(slot + 1), stride(stride_), batch(a.batch), q(a.queue), tk(0), tlen(1), seen(0) {}
+  __device__ __forceinline__ void prefetch(int sl) {
+    if (q && hs + 1 == end) {
+      const long long rem = batch - stride - (long long)seen;
+      long long len = rem / (4 * stride);
+      len = len < 1 ? 1 : (len > 64 ? 64 : len);
+      tlen = (uint32_t)len;
+      if (sl == 0) tk = atomicAdd(q, tlen);
+    }
+  }
+  __device__ __forceinline__ void advance(int leader) {
+    if (!q) {
+      hs += stride;
+      return;
+    }
+    hs += 1;
+    if (hs < end) return;
+    const uint32_t t = (uint32_t)__shfl((int)tk, leader, 64);
+    seen = t + tlen;
+    hs = stride + (long long)t;
+    end = hs + tlen;
+  }
+};
+
+template <int K, int LPH>
+__device__ __forceinline__ uint32_t vn_layer_grp(const uint32_t* adj_info, const uint32_t* avar, float* colS,
+                                                 const float* c2v, int v0, int nadj, int pa, int sl, float thr) {
+  uint32_t acc = 0;
+  for (int cb = 0; cb < pa; cb += 2 * LPH) {
+    uint32_t info[2];
+    bool in[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int i = cb + h * LPH + sl;
+      in[h] = i < nadj;
+      info[h] = adj_info[v0 + (in[h] ? i : 0)];
+    }
+    float old[2];
+    uint32_t av[2];
+    float x[2][K];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      old[h] = colS[info[h] >> 21];
+      av[h] = avar[info[h] >> 21];
+      const float* c = c2v + (info[h] & 0xffffu);
+#pragma unroll
+      for (int t = 0; t < K; ++t) x[h][t] = c[t];
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int d = (int)((info[h] >> 16) & 31u);
+      float s = 0.0f;                                       // sequential, ascending check (:172)
+#pragma unroll
+      for (int t = 0; t < K; ++t) s += (t < d) ? x[h][t] : 0.0f;
+      if (in[h]) colS[info[h] >> 21] = s;
+      const bool flip = in[h] && ((old[h] < thr) != (s < thr));
+      acc ^= flip ? av[h] : 0u;
+    }
+  }
+  return acc;
+}
+
+template <int DC, int NH, int G>
+__global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_grp_kernel(DecodeArgs a) {
+  constexpr int LPH = 64 / NH;
+  constexpr int CPP = LPH / G;                                  // checks per CN pass per group
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  {
+    const uint4* src = (const uint4*)a.blob;
+    uint4* dst = (uint4*)lds;
+    const int nvec = a.blob_bytes >> 4;
+    for (int i = threadIdx.x; i < nvec; i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  const uint32_t* ltab = (const uint32_t*)(lds + a.off_cn_tab);      // [Q][8]
+  const uint16_t* lrow = (const uint16_t*)(lds + a.off_lay_rows);    // [Q]
+  const uint16_t* lay_ptr = (const uint16_t*)(lds + a.off_lay_ptr);  // [L+1]
+  const uint16_t* adj_ptr = (const uint16_t*)(lds + a.off_adj_ptr);  // [L+1]
+  const uint32_t* adj_info = (const uint32_t*)(lds + a.off_row_ptr); // [A] var<<21 | deg<<16 | csc start
+  const uint8_t* adj_dmax = (const uint8_t*)(lds + a.off_chunk_dmax);// [L]
+  const uint32_t* avar = (const uint32_t*)(lds + a.off_vn_chk);      // [n] filter words
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int waves = blockDim.x >> 6;
+  const int grp = lane / LPH, sl = lane % LPH, leader = grp * LPH;
+  const uint64_t gmask = group_mask<LPH>(grp);
+  // this group's half-shot slice: colS f32[n] | c2v f32[E + 8] | syndrome u8[m]
+  unsigned char* ws = lds + a.blob_bytes + (wid * NH + grp) * a.wave_bytes;
+  float* colS = (float*)ws;
+  unsigned char* c2v_b = ws + a.off_c2v;
+  float* c2v = (float*)c2v_b;
+  uint8_t* synb = ws + a.off_synw;
+  const uint32_t post_b = lds_addr(colS), c2v_a = lds_addr(c2v_b);
+  const int m = a.m, n = a.n, nl = a.n_layers;
+  const float thr = a.hd_thresh;
+  const double L = a.L;
+
+  GroupQueue Q(a, ((long long)blockIdx.x * waves + wid) * NH + grp, (long long)gridDim.x * waves * NH);
+  bool active = false;
+  int lay = 0, it = 0, fl = 0;
+  bool first = true;
+  uint32_t F = 0, B = 0;
+
+  // starts half-shot Q.hs in this group's slice (lanes of starting groups only)
+  auto start = [&]() {
+    const uint8_t* syn = a.syn + Q.hs * (long long)m;
+    for (int c = sl; c < m; c += LPH) synb[c] = syn[c] & 1;
+    for (int j = sl; j < n; j += LPH) colS[j] = 0.0f;            // post = L, c2v = 0 (:148-150)
+    for (int p = sl; p < a.E; p += LPH) c2v[p] = 0.0f;
+    lay = 0;
+    it = 0;
+    fl = 0;
+    first = true;
+    F = (L < 0.0) ? a.filt_all : 0u;
+  };
+
+  active = Q.hs < a.batch;
+  if (active) {
+    Q.prefetch(sl);
+    start();
+  }
+  wave_sync();
+  {
+    uint32_t b = 0;
+    if (active)
+      for (int c = sl; c < m; c += LPH) b ^= synb[c] ? a.wc[c] : 0u;
+    B = group_xor<LPH>(b, grp);
+  }
+
+  while (ballot(active) != 0) {
+    // ---- check nodes of each group's current layer (Jacobi, :155-169)
+    const int q0 = lay_ptr[lay], q1 = lay_ptr[lay + 1];
+    const int rows = active ? q1 - q0 : 0;
+    const int prow = groups_max<LPH>(rows);
+    for (int qb = 0; qb < prow; qb += CPP) {
+      const int qi = qb + sl / G;
+      const bool live = qi < rows;
+      const int qs = q0 + (live ? qi : 0);
+      const int c = lrow[qs];
+      cn_ms_split<DC, G>(a, ltab + qs * 8, sl & (G - 1), live, (uint32_t)synb[c], first, post_b, c2v_a, fl);
+    }
+    first = false;
+    wave_sync();
+    // ---- variable nodes adjacent to the layer (:172-174)
+    const int v0 = adj_ptr[lay], v1 = adj_ptr[lay + 1];
+    const int nadj = active ? v1 - v0 : 0;
+    const int pa = groups_max<LPH>(nadj);
+    const int kmax = groups_max<LPH>(active ? ((int)adj_dmax[lay] & 31) : 0);
+    uint32_t acc = 0;
+    switch (kmax) {
+      case 3: acc = vn_layer_grp<3, LPH>(adj_info, avar, colS, c2v, v0, nadj, pa, sl, thr); break;
+      case 4: acc = vn_layer_grp<4, LPH>(adj_info, avar, colS, c2v, v0, nadj, pa, sl, thr); break;
+      case 5: acc = vn_layer_grp<5, LPH>(adj_info, avar, colS, c2v, v0, nadj, pa, sl, thr); break;
+      case 6: acc = vn_layer_grp<6, LPH>(adj_info, avar, colS, c2v, v0, nadj, pa, sl, thr); break;
+      default:
+        for (int i = sl; i < pa; i += LPH) {
+          if (i < nadj) {
+            const uint32_t info = adj_info[v0 + i];
+            const int j = (int)(info >> 21), d = (int)((info >> 16) & 31u);
+            const float old = colS[j];
+            const float s = ms_colsum_sw(c2v + (info & 0xffffu), d, kmax);
+            colS[j] = s;
+            if ((old < thr) != (s < thr)) acc ^= avar[j];
+          }
+        }
+    }
+    F ^= group_xor<LPH>(acc, grp);
+    wave_sync();
+    // ---- stop test (:175-176): filters, then the exact test for groups that pass
+    const bool cand = active && F == B;
+    bool conv = false;
+    if (ballot(cand) != 0) {
+      uint32_t un = 0;
+      if (cand) {
+        for (int c = sl; c < m; c += LPH) {
+          const uint4 t0 = *(const uint4*)(a.rtab + 8 * (size_t)c);
+          const uint4 t1 = *(const uint4*)(a.rtab + 8 * (size_t)c + 4);
+          const uint32_t t[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+          uint32_t par = 0;
+#pragma unroll
+          for (int k = 0; k < DC; ++k) par ^= (uint32_t)(colS[t[k]] < thr);
+          un |= par ^ (uint32_t)synb[c];
+        }
+      }
+      conv = cand && (ballot(un != 0) & gmask) == 0;
+    }
+    const bool done = active && (conv || (lay + 1 == nl && it + 1 == a.max_iter));
+    if (active && !done) {
+      if (++lay == nl) {
+        lay = 0;
+        ++it;
+      }
+    }
+    if (ballot(done) != 0) {
+      const bool fmz = (ballot((fl & FLAG_MIN_ZERO) != 0) & gmask) != 0;
+      if (done) {
+        // ê and posteriors in original column order
+        const long long hs = Q.hs;
+        uint8_t* eh = a.ehat + hs * (long long)n;
+        double* po = a.post ? a.post + hs * (long long)n : nullptr;
+        for (int jo = sl; jo < n; jo += LPH) {
+          const double pv = L + (double)colS[a.vinv[jo]];
+          eh[jo] = (uint8_t)(pv < 0.0);
+          if (po) po[jo] = pv;
+        }
+        if (sl == 0) {
+          a.iters[hs] = conv ? it + 1 : a.max_iter;
+          if (a.flags) a.flags[hs] = (int32_t)((fmz ? FLAG_MIN_ZERO : 0) | (conv ? FLAG_CONVERGED : 0));
+        }
+        Q.advance(leader);
+        active = Q.hs < a.batch;
+      }
+      wave_sync();                                               // slice reuse
+      const bool restart = done && active;
+      if (restart) {
+        Q.prefetch(sl);
+        start();
+      }
+      wave_sync();
+      if (ballot(restart) != 0) {
+        uint32_t b = 0;
+        if (restart)
+          for (int c = sl; c < m; c += LPH) b ^= synb[c] ? a.wc[c] : 0u;
+        const uint32_t nb = group_xor<LPH>(b, grp);
+        if (restart) B = nb;
+      }
+    }
   }
 }
 
@@ -1638,9 +1946,20 @@ const void* select_bp_team_kernel(bool layered, int dc, int w, const char** name
 
 const void* select_ms_layered_kernel(int dc, int g, const char** name) {
 #define QLDPC_MSL(D, Gn) if (dc == D && g == Gn) QLDPC_NAMED((&ms_layered_kernel<D, Gn>), "ms_layered_kernel<" #D ", " #Gn ">");
-  QLDPC_MSL(7, 1) QLDPC_MSL(8, 1) QLDPC_MSL(7, 2) QLDPC_MSL(8, 2)
+  QLDPC_MSL(7, 0) QLDPC_MSL(8, 0) QLDPC_MSL(7, 1) QLDPC_MSL(8, 1) QLDPC_MSL(7, 2) QLDPC_MSL(8, 2)
   QLDPC_MSL(7, 4) QLDPC_MSL(8, 4) QLDPC_MSL(7, 8) QLDPC_MSL(8, 8)
 #undef QLDPC_MSL
+  return nullptr;
+}
+
+const void* select_ms_layered_grp_kernel(int dc, int nh, int g, const char** name) {
+#define QLDPC_MSG(D, N, Gn)            \
+  if (dc == D && nh == N && g == Gn) \
+    QLDPC_NAMED((&ms_layered_grp_kernel<D, N, Gn>), "ms_layered_grp_kernel<" #D ", " #N ", " #Gn ">");
+  QLDPC_MSG(7, 2, 1) QLDPC_MSG(8, 2, 1) QLDPC_MSG(7, 2, 2) QLDPC_MSG(8, 2, 2)
+  QLDPC_MSG(7, 4, 1) QLDPC_MSG(8, 4, 1) QLDPC_MSG(7, 4, 2) QLDPC_MSG(8, 4, 2)
+  QLDPC_MSG(7, 1, 1) QLDPC_MSG(8, 1, 1) QLDPC_MSG(7, 1, 4) QLDPC_MSG(8, 1, 4)
+#undef QLDPC_MSG
   return nullptr;
 }
 

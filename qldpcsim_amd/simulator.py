@@ -185,6 +185,12 @@ def _device_ok():
         return False
 
 
+def _channel_ok(Hx, Hz):
+    """The device sampler / counters handle n <= 4096 qubits (64 error words
+    per shot, qldpc_channel_sample); larger codes use the host sampler."""
+    return Hx.shape[1] <= 4096 and Hx.shape[1] == Hz.shape[1]
+
+
 def _dist():
     try:
         import torch.distributed as dist
@@ -235,7 +241,13 @@ def simulate_p(Hx: np.ndarray, Hz: np.ndarray, p: float, shots: int = 1000, decT
     tot = {k: 0 for k in COUNTER_KEYS}
     t0 = time.time()
     done = 0
-    use_dev = sampler == "device" or (sampler is None and samples is None and _device_ok())
+    if sampler not in (None, "device", "host"):
+        raise ValueError("sampler must be 'device', 'host' or None")
+    if samples is not None and sampler == "device":
+        raise ValueError("samples= decodes the given shots on the host path; it cannot be combined "
+                         "with sampler='device' (which draws its own Philox shots)")
+    use_dev = sampler == "device" or (sampler is None and samples is None and _device_ok()
+                                      and _channel_ok(Hx, Hz))
     if batch_size is None:
         # shots per batch. Without OSD nothing syncs per batch, and 2^20-shot
         # batches amortise the per-batch host work (LP118_0 MS-F p = 0.01:
@@ -372,9 +384,11 @@ def simulate(HxFile: str, HzFile: str, p, shots: int = 1000, decType: str = "MS"
     Hz = load_matrix(HzFile)
     assert max(p) <= 1. and min(p) >= 0.
     _, rank, world = _dist()
+    if sampler is None:                       # the resolved shot source is part of the run
+        sampler = "device" if (_device_ok() and _channel_ok(Hx, Hz)) else "host"
     meta = {"Hx": HxFile, "Hz": HzFile, "shots": shots, "decType": decType,
             "decIterations": decIterations, "decSchedule": decSchedule, "OSDorder": OSDorder,
-            "rngSeed": rngSeed, "world": world}
+            "rngSeed": rngSeed, "world": world, "sampler": sampler}
     done = _load_results(resultsFile, meta)
     results = []
     for pT in p:
@@ -432,7 +446,8 @@ def main(argv=None):
                         help="Decoder scheduling method: [F] flooding; [L] layered; [S] serial.")
     parser.add_argument("--OSDorder", type=int, default=-1, help="Ordered Statistics Decoding order.")
     parser.add_argument("--batch", type=int, default=None,
-                        help="Shots per batch (default 2^18 on the GPU, 2^16 on the host path).")
+                        help="Shots per batch (default on the GPU: 2^20 without OSD, 2^18 with OSD; "
+                             "2^16 on the host path).")
     parser.add_argument("--sampler", choices=["device", "host"], default=None,
                         help="Where shots are sampled and counted (default: device if present).")
     parser.add_argument("--results", default=None,

@@ -203,36 +203,80 @@ def test_decode_batch_into_preallocated_buffers(dec):
 
 
 
-@pytest.mark.parametrize("kernel", ["G1", "G2", "G4", "G8", "generic"])
-def test_ms_layered_kernels_match_oracle(dec, kernel, monkeypatch):
-    """ms_layered_kernel at every lanes-per-check width G (QLDPC_MS_LANES_PER_CHECK;
-    the default picks one from the median layer) and the generic decode kernel
-    (QLDPC_NO_LAYERED_FAST) against the oracle, bit for bit, on LP118_2 with
-    fixed-work and channel syndromes: G changes which lanes own which edges,
-    never the arithmetic."""
+KERNELS = ["G1", "G2", "G4", "G8", "generic", "default", "N1G4", "N2G1", "N2G2", "N4G1", "N4G2"]
+
+
+@pytest.mark.parametrize("code", ["LP118_2", "LP118_0", "LP04_0"])
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_ms_layered_kernels_match_oracle(dec, kernel, code, monkeypatch):
+    """Every layered MS kernel shape against the oracle, bit for bit, with
+    fixed-work and channel syndromes mixed in one batch (so lane groups of
+    ms_layered_grp_kernel finish at different layers and restart): the
+    one-half-shot-per-wave ms_layered_kernel at every lanes-per-check width G
+    (QLDPC_MS_GROUPS=1, QLDPC_MS_LANES_PER_CHECK), ms_layered_grp_kernel with
+    NH half-shots per wave and G lanes per check (QLDPC_MS_GROUPS,
+    QLDPC_MS_GRP_G), the default choice, and the generic decode kernel
+    (QLDPC_NO_LAYERED_FAST). Lane mappings never change the arithmetic."""
     from oracle import oracle
     from qldpcsim_amd import _lib, codes, schedule
-    Hx, Hz = codes.load_code("LP118_2")
+    Hx, Hz = codes.load_code(code)
     if kernel == "generic":
         monkeypatch.setenv("QLDPC_NO_LAYERED_FAST", "1")
-    else:
+    elif kernel.startswith("G"):
+        monkeypatch.setenv("QLDPC_MS_GROUPS", "1")
         monkeypatch.setenv("QLDPC_MS_LANES_PER_CHECK", kernel[1:])
+    elif kernel.startswith("N"):
+        monkeypatch.setenv("QLDPC_MS_GROUPS", kernel[1])
+        monkeypatch.setenv("QLDPC_MS_GRP_G", kernel[3:])
     lx, _ = schedule.select_layers(Hx, Hz, "L")
     lp, lr = schedule.pack_layers(lx, Hz.shape[0])
     rng = np.random.default_rng(11)
     syn = np.concatenate([rng.integers(0, 2, (128, Hz.shape[0]), dtype=np.uint8),
                           _channel(Hx, Hz, 0.06, 256, 5)[0]])
-    code = _lib.code_for(Hz)
-    code._sched.clear()                  # launch configs read the env once per schedule
+    syn = syn[rng.permutation(len(syn))]
+    code_h = _lib.code_for(Hz)
+    code_h._sched.clear()                  # launch configs read the env once per schedule
     try:
         r = dec.decode_batch(Hz, syn, 0.06 / 3, 30, algo="MS", want_post=True, layer_ptr=lp, layer_rows=lr)
+        if kernel.startswith("N"):
+            nm = _lib.kernel_name(Hz, lp, lr, "MS")
+            assert nm.startswith("ms_layered_grp_kernel<") and nm.endswith(f", {kernel[1]}, {kernel[3:]}>"), nm
     finally:
-        code._sched.clear()
+        code_h._sched.clear()
     e, it, post, fl = oracle.decode_batch("MS", Hz, syn, 0.06 / 3, 30, lp, lr)
     np.testing.assert_array_equal(r.iters, it)
     np.testing.assert_array_equal(r.ehat, e)
     np.testing.assert_array_equal(r.post.view(np.uint64), post.view(np.uint64))
     np.testing.assert_array_equal((r.flags & 2) != 0, (fl & 1) != 0)
+
+
+@pytest.mark.parametrize("groups", ["1", "2"])
+def test_ms_layered_large_mixed_batch(dec, groups, monkeypatch):
+    """The default layered kernel and ms_layered_grp_kernel (QLDPC_MS_GROUPS=2)
+    over a batch large enough that the work queue hands out multi-half-shot
+    chunks, with decodes of very different lengths: bit-exact vs the oracle."""
+    from oracle import oracle
+    from qldpcsim_amd import _lib, codes, schedule
+    Hx, Hz = codes.load_code("LP118_0")
+    _, lz = schedule.select_layers(Hx, Hz, "L")
+    lp, lr = schedule.pack_layers(lz, Hx.shape[0])
+    monkeypatch.setenv("QLDPC_MS_GROUPS", groups)
+    code_h = _lib.code_for(Hx)
+    code_h._sched.clear()
+    rng = np.random.default_rng(3)
+    syn = np.concatenate([rng.integers(0, 2, (3000, Hx.shape[0]), dtype=np.uint8),
+                          _channel(Hx, Hz, 0.04, 30000, 8)[1]])
+    syn = syn[rng.permutation(len(syn))]
+    try:
+        nm = _lib.kernel_name(Hx, lp, lr, "MS")
+        assert nm.startswith("ms_layered_grp_kernel" if groups == "2" else "ms_layered_kernel<8, 0>"), nm
+        r = dec.decode_batch(Hx, syn, 0.04 / 3, 40, algo="MS", want_post=True, layer_ptr=lp, layer_rows=lr)
+    finally:
+        code_h._sched.clear()
+    e, it, post, fl = oracle.decode_batch("MS", Hx, syn, 0.04 / 3, 40, lp, lr)
+    np.testing.assert_array_equal(r.iters, it)
+    np.testing.assert_array_equal(r.ehat, e)
+    np.testing.assert_array_equal(r.post.view(np.uint64), post.view(np.uint64))
 
 
 @pytest.mark.parametrize("sched", ["L", "S"])

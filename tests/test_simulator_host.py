@@ -187,3 +187,34 @@ def test_resumable_results_file(tmp_path, monkeypatch):
     with pytest.raises(ValueError):
         simulator.simulate(str(tmp_path / "Hx.npy"), str(tmp_path / "Hz.npy"), [0.01],
                            **{**kw, "shots": 200})
+
+
+def test_samples_with_device_sampler_is_rejected():
+    from qldpcsim_amd import codes, simulator
+    Hx, Hz = codes.load_code("steane")
+    smp = simulator.sample_channel(Hx, Hz, 0.1, 4, np.random.default_rng(0))
+    with pytest.raises(ValueError):
+        simulator.simulate_p(Hx, Hz, 0.1, shots=4, samples=smp, sampler="device", verbose=False)
+    with pytest.raises(ValueError):
+        simulator.simulate_p(Hx, Hz, 0.1, shots=4, samples=smp, sampler="gpu", verbose=False)
+
+
+def test_results_file_records_the_sampler(tmp_path):
+    """A resumed sweep must not mix host-stream and device-stream p-points:
+    the resolved sampler is part of the results file's run parameters."""
+    import json
+    from qldpcsim_amd import simulator
+    path = str(tmp_path / "res.json")
+    meta = {"Hx": "a", "Hz": "b", "shots": 10, "decType": "MS", "decIterations": 5, "decSchedule": "F",
+            "OSDorder": -1, "rngSeed": 1, "world": 1, "sampler": "device"}
+    simulator._save_results(path, meta, {0.1: {"decSuccessExact": 3}})
+    assert simulator._load_results(path, meta) == {0.1: {"decSuccessExact": 3}}
+    with pytest.raises(ValueError):
+        simulator._load_results(path, dict(meta, sampler="host"))
+    assert json.load(open(path))["meta"]["sampler"] == "device"
+
+
+def test_large_codes_use_the_host_sampler():
+    from qldpcsim_amd import simulator
+    assert simulator._channel_ok(np.zeros((3, 4096)), np.zeros((3, 4096)))
+    assert not simulator._channel_ok(np.zeros((3, 4097)), np.zeros((3, 4097)))
