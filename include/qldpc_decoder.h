@@ -139,6 +139,28 @@ int qldpc_osd_device(const qldpc_code *code, int64_t count, const uint8_t *d_syn
                      const int32_t *d_perm, int order, uint8_t *d_ehat, int32_t *d_status,
                      void *stream);
 
+/* The reliability order of decoders.py:320-325 on the device, for `count`
+ * posterior rows d_post double[count][n] (n <= 2048): d_perm int32[count][n]
+ * = the keys max(prob, 1 - prob), prob = 1/(1 + exp(clip(post, +-100))),
+ * sorted ascending (index order among equal keys). NumPy's argsort orders
+ * equal keys its own way and NumPy's exp may differ from the device's in the
+ * last bits, so the order is only certified below d_tiepos[row]: the first
+ * sorted position whose key gap to the next is within 64 units in the last
+ * place (n if none; 0 if a posterior is NaN). No reference counterpart as an
+ * entry point (it replaces the np.argsort call inside OSDdec). */
+int qldpc_osd_order_device(const qldpc_code *code, int64_t count, const double *d_post, int32_t *d_perm,
+                           int32_t *d_tiepos, void *stream);
+
+/* qldpc_osd_device with the order computed on the device
+ * (qldpc_osd_order_device into the caller's workspaces d_perm / d_tiepos):
+ * a shot whose result depends on a part of the order that is not certified
+ * (its elimination visited position tiepos, or the order-1 flip lies there)
+ * gets d_status 2 and its e_hat is left unchanged: the caller decides it with
+ * NumPy's order (qldpc_osd_device). Status 0 / 1 as qldpc_osd_device. */
+int qldpc_osd_device_ordered(const qldpc_code *code, int64_t count, const uint8_t *d_syn, const double *d_post,
+                             int order, uint8_t *d_ehat, int32_t *d_status, int32_t *d_perm, int32_t *d_tiepos,
+                             void *stream);
+
 /* First element of CPython's `set(range(n)) - set(J)` iteration order
  * (the reference's infoSet[0], decoders.py:344); -1 if empty. */
 int qldpc_cpython_setdiff_first(int n, const int32_t *J, int nJ);

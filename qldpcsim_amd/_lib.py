@@ -23,7 +23,8 @@ EXPORTS = (
     "qldpc_code_create", "qldpc_code_destroy", "qldpc_code_shape",
     "qldpc_schedule_create", "qldpc_schedule_destroy",
     "qldpc_decode_device", "qldpc_decode_host", "qldpc_decode_kernel_name",
-    "qldpc_osd_decode", "qldpc_osd_decode_batch", "qldpc_osd_device", "qldpc_cpython_setdiff_first",
+    "qldpc_osd_decode", "qldpc_osd_decode_batch", "qldpc_osd_device", "qldpc_osd_order_device",
+    "qldpc_osd_device_ordered", "qldpc_cpython_setdiff_first",
     "qldpc_channel_thresholds", "qldpc_channel_sample", "qldpc_count_outcomes",
     "qldpc_timing_enable", "qldpc_timing_reset", "qldpc_timing_read",
 )
@@ -65,6 +66,8 @@ def _load():
         "qldpc_osd_decode": ([P, P, P, I, P, P, P, I], I),
         "qldpc_osd_decode_batch": ([P, I64, P, P, I, P, I], I),
         "qldpc_osd_device": ([P, I64, P, P, I, P, P, P], I),
+        "qldpc_osd_order_device": ([P, I64, P, P, P, P], I),
+        "qldpc_osd_device_ordered": ([P, I64, P, P, I, P, P, P, P, P], I),
         "qldpc_cpython_setdiff_first": ([I, P, I], I),
         "qldpc_channel_thresholds": ([D, P, P, P], I),
         "qldpc_channel_sample": ([P, P, D, ctypes.c_uint64, ctypes.c_uint64, I64, P, P, P, P, P], I),

@@ -1126,9 +1126,47 @@ static int setdiff_table_ints(int n) {
   return (int)best;
 }
 
+static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t* d_syn, const int32_t* d_perm,
+                           const int32_t* d_tiepos, int order, uint8_t* d_ehat, int32_t* d_status,
+                           void* stream);
+
 extern "C" int qldpc_osd_device(const qldpc_code* code, int64_t count, const uint8_t* d_syn,
                                 const int32_t* d_perm, int order, uint8_t* d_ehat, int32_t* d_status,
                                 void* stream) {
+  return osd_device_impl(code, count, d_syn, d_perm, nullptr, order, d_ehat, d_status, stream);
+}
+
+extern "C" int qldpc_osd_order_device(const qldpc_code* code, int64_t count, const double* d_post,
+                                      int32_t* d_perm, int32_t* d_tiepos, void* stream) {
+  if (!code) return fail(QLDPC_EINVAL, "code is null");
+  if (count < 0) return fail(QLDPC_EINVAL, "negative count");
+  if (count == 0) return QLDPC_OK;
+  if (code->device < 0) return fail(QLDPC_EHIP, "no HIP device was visible when the code was created");
+  if (!d_post || !d_perm || !d_tiepos) return fail(QLDPC_EINVAL, "null device buffer");
+  const int n = code->n;
+  if (n < 1 || n > 2048) return fail(QLDPC_EUNSUP, "the device reliability order supports 1 <= n <= 2048 (got %d)", n);
+  qldpc::OrderArgs a{};
+  a.post = d_post;
+  a.perm = d_perm;
+  a.tiepos = d_tiepos;
+  a.n = n;
+  a.np2 = 2;
+  while (a.np2 < n) a.np2 <<= 1;
+  HIP_TRY(qldpc::launch_osd_order(a, count, (hipStream_t)stream));
+  return QLDPC_OK;
+}
+
+extern "C" int qldpc_osd_device_ordered(const qldpc_code* code, int64_t count, const uint8_t* d_syn,
+                                        const double* d_post, int order, uint8_t* d_ehat, int32_t* d_status,
+                                        int32_t* d_perm, int32_t* d_tiepos, void* stream) {
+  int rc = qldpc_osd_order_device(code, count, d_post, d_perm, d_tiepos, stream);
+  if (rc != QLDPC_OK) return rc;
+  return osd_device_impl(code, count, d_syn, d_perm, d_tiepos, order, d_ehat, d_status, stream);
+}
+
+static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t* d_syn, const int32_t* d_perm,
+                           const int32_t* d_tiepos, int order, uint8_t* d_ehat, int32_t* d_status,
+                           void* stream) {
   if (!code) return fail(QLDPC_EINVAL, "code is null");
   if (count < 0) return fail(QLDPC_EINVAL, "negative count");
   if (count == 0) return QLDPC_OK;
@@ -1158,6 +1196,7 @@ extern "C" int qldpc_osd_device(const qldpc_code* code, int64_t count, const uin
   a.n = n;
   a.rank = code->rank;
   a.order = order;
+  a.tiepos = d_tiepos;
   const int block = std::max(64, (m + 63) / 64 * 64);
   int64_t done = 0;
   while (done < count) {  // grid.x limit
@@ -1167,6 +1206,7 @@ extern "C" int qldpc_osd_device(const qldpc_code* code, int64_t count, const uin
     ai.syn = d_syn + done * m;
     ai.ehat = d_ehat + done * n;
     ai.status = d_status + done;
+    if (ai.tiepos) ai.tiepos = d_tiepos + done;
     void* params[] = {(void*)&ai};
     HIP_TRY(hipLaunchKernel(k, dim3((unsigned)g), dim3(block), params, (size_t)lds, (hipStream_t)stream));
     done += g;

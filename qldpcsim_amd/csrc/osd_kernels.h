@@ -11,9 +11,26 @@ struct OsdArgs {
   const int32_t* perm;     // [count][n] reliability order (NumPy argsort, decoders.py:325)
   const uint8_t* syn;      // [count][m]
   uint8_t* ehat;           // [count][n] in/out
-  int32_t* status;         // [count] 0 ok, 1 = reference IndexError case
+  int32_t* status;         // [count] 0 ok, 1 = reference IndexError case, 2 = order not certified
+  const int32_t* tiepos;   // [count] or null: first sorted position t whose key gap to t+1 is
+                           // within the certification margin (osd_order_kernel); with it, a
+                           // shot whose decision prefix reaches tiepos is left untouched (status 2)
   int m, n, rank, order;
 };
+
+// Reliability order on the device (decoders.py:320-325): keys
+// max(prob, 1 - prob), prob = 1 / (1 + exp(clip(post, +-100))), sorted
+// ascending (index order among equal keys) into perm; tiepos = the first
+// sorted position whose gap to the next key is <= kOrderMarginUlp units in
+// the last place (n if none, 0 for a non-finite posterior).
+struct OrderArgs {
+  const double* post;      // [count][n]
+  int32_t* perm;           // [count][n]
+  int32_t* tiepos;         // [count]
+  int n, np2;              // np2 = power of two >= n (<= 2048)
+};
+constexpr int kOrderMarginUlp = 64;
+hipError_t launch_osd_order(const OrderArgs& a, long long count, hipStream_t stream);
 
 const void* select_osd_kernel(int nw);  // nw = 64-bit words per row incl. the syndrome column
 int osd_nw_of(int nw);

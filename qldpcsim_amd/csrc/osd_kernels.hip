@@ -162,6 +162,22 @@ __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
     return;
   }
   __syncthreads();
+  if (a.tiepos) {
+    // device-computed order: the result depends only on perm[0 .. need]
+    // (the columns the elimination visited and, for order 1, the flipped
+    // position); it equals NumPy's order there unless a key gap inside that
+    // prefix is within the certification margin -> leave it to the host
+    if (t == 0) {
+      int need = Jl[nJ - 1];
+      if (a.order == 1 && nJ < n) need = max(need, first_setdiff(n, inJ, nJ, table));
+      misc[3] = a.tiepos[shot] <= need;
+    }
+    __syncthreads();
+    if (misc[3]) {
+      if (t == 0) a.status[shot] = 2;
+      return;
+    }
+  }
   // information-set values e_I (e_perm = e_hat[perm], decoders.py:345):
   // one column per thread, words assembled by ballots (all loads in flight)
   for (int i0w = 64 * wave; i0w < 64 * NW; i0w += blockDim.x) {
@@ -194,6 +210,86 @@ __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
   }
   if (t == 0 && i0 >= 0) ehat[perm[i0]] ^= 1;
   if (t == 0) a.status[shot] = 0;
+}
+
+// ---------------------------------------------------------------------------
+// Reliability order of one shot per workgroup (np2 / 2 threads): keys as
+// NumPy forms them in decoders.py:320-325 (clip, exp, 1 / (1 + e),
+// max(prob, 1 - prob)), with the device exp; a key lies in [0.5, 1], so
+// (bits - bits(0.5)) fits 53 bits and (that << 11 | index) sorts by key, then
+// index, as one 64-bit integer (bitonic network in LDS). NumPy's argsort
+// breaks ties its own way and its exp may differ from the device's in the
+// last bits, so the caller trusts this order only up to tiepos (the first
+// adjacent pair closer than kOrderMarginUlp units in the last place).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) osd_order_kernel(OrderArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  uint64_t* key = (uint64_t*)lds;                   // [np2]
+  int* tmin = (int*)(lds + 8 * a.np2);               // [1]
+  const int t = threadIdx.x, nt = blockDim.x;
+  const long long shot = blockIdx.x;
+  const double* post = a.post + shot * (long long)a.n;
+  const int n = a.n, np2 = a.np2;
+  constexpr uint64_t kHalf = 0x3FE0000000000000ull;  // bits of 0.5
+  bool bad = false;
+  for (int i = t; i < np2; i += nt) {
+    uint64_t c = ~0ull;                               // padding sorts last
+    if (i < n) {
+      double x = post[i];
+      x = x < -100.0 ? -100.0 : (x > 100.0 ? 100.0 : x);   // np.clip(P, -100, 100)
+      const double e = exp(x);
+      const double prob = 1.0 / (1.0 + e);
+      const double q = 1.0 - prob;
+      const double rel = prob > q ? prob : q;         // np.maximum(prob, 1 - prob)
+      if (!(rel >= 0.5 && rel <= 1.0)) bad = true;    // NaN posterior: host decides
+      const uint64_t u = (__builtin_bit_cast(uint64_t, rel) - kHalf) & ((1ull << 53) - 1);
+      c = (u << 11) | (uint64_t)i;
+    }
+    key[i] = c;
+  }
+  if (t == 0) *tmin = n;
+  __syncthreads();
+  for (int k = 2; k <= np2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = t; i < np2 / 2; i += nt) {
+        const int lo = 2 * i - (i & (j - 1)), hi = lo + j;
+        const bool up = (lo & k) == 0;
+        const uint64_t x = key[lo], y = key[hi];
+        if ((x > y) == up) {
+          key[lo] = y;
+          key[hi] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  int first = bad ? 0 : n;
+  for (int i = t; i + 1 < n; i += nt)
+    if ((key[i + 1] >> 11) - (key[i] >> 11) <= (uint64_t)kOrderMarginUlp) first = min(first, i);
+  for (int off = 32; off > 0; off >>= 1) first = min(first, __shfl_xor(first, off, 64));
+  if ((t & 63) == 0) atomicMin(tmin, first);
+  int32_t* perm = a.perm + shot * (long long)n;
+  for (int i = t; i < n; i += nt) perm[i] = (int32_t)(key[i] & 2047u);
+  __syncthreads();
+  if (t == 0) a.tiepos[shot] = *tmin;
+}
+
+hipError_t launch_osd_order(const OrderArgs& a, long long count, hipStream_t stream) {
+  long long done = 0;
+  while (done < count) {
+    const long long g = count - done < (1ll << 30) ? count - done : (1ll << 30);
+    OrderArgs ai = a;
+    ai.post = a.post + done * a.n;
+    ai.perm = a.perm + done * a.n;
+    ai.tiepos = a.tiepos + done;
+    void* params[] = {(void*)&ai};
+    const size_t lds = (size_t)8 * a.np2 + 16;
+    hipError_t e = hipLaunchKernel((const void*)&osd_order_kernel, dim3((unsigned)g), dim3(a.np2 / 2), params,
+                                   lds, stream);
+    if (e != hipSuccess) return e;
+    done += g;
+  }
+  return hipSuccess;
 }
 
 // CPython setobject.c emulation (set_difference -> set_add_entry with

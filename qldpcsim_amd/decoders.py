@@ -191,29 +191,38 @@ def _pinned(key, shape, dtype):
 
 
 def apply_osd_device(H, syn, res, order, stream=None):
-    """GPU OSD (qldpc_osd_device) for the non-converged shots of a device
-    decode `res` (DecodeResult of torch tensors, with posteriors): only their
-    posteriors travel to the host (pinned, asynchronous) for NumPy's
-    reliability order; the GF(2) work runs on the GPU. Updates res.ehat in
-    place. See apply_osd_device_many for several decodes at once."""
+    """GPU OSD for the non-converged shots of a device decode `res`
+    (DecodeResult of torch tensors, with posteriors). The reliability order is
+    computed on the device and trusted where it provably equals NumPy's
+    (qldpc_osd_device_ordered); only the shots whose OSD depends on a near-tie
+    have their posteriors copied to the host for NumPy's own order. Updates
+    res.ehat in place. See apply_osd_device_many for several decodes at once."""
     return apply_osd_device_many([(H, syn, res)], order, stream)[0]
 
 
 def apply_osd_device_many(items, order, stream=None):
     """apply_osd_device for several (H, syn, res) decodes (the X and Z halves
-    of a batch): every posterior copy is queued first, so the next copy runs
-    while the host computes the previous one's reliability order."""
-    staged = osd_device_stage(items, stream)
+    of a batch): every device order and elimination is queued first."""
+    staged = osd_device_stage(items, stream, order=order)
     osd_device_finish(items, staged, order, stream)
     osd_status_check(items)
     return [r.ehat for _, _, r in items]
 
 
-def osd_device_stage(items, stream=None, slot0=0):
+def _host_order_only():
+    import os
+    return os.environ.get("QLDPC_OSD_HOST_ORDER", "") == "1"
+
+
+def osd_device_stage(items, stream=None, slot0=0, order=0):
     """First half of the device OSD: find each decode's non-converged shots
-    (one device sync) and queue the asynchronous copy of their posteriors into
-    pinned host buffers. Returns the staging records for osd_device_finish.
-    `slot0` selects the pinned buffer set (pipelined callers alternate)."""
+    (one device sync), then queue asynchronously on the device: the
+    reliability order (decoders.py:320-325) and the elimination of every shot
+    whose result the device order decides, with its status copied into a
+    pinned host buffer. Shots that need NumPy's order (status 2) are finished
+    by osd_device_finish. `slot0` selects the pinned buffer set (pipelined
+    callers alternate). QLDPC_OSD_HOST_ORDER=1 (A/B only) or n > 2048 sends
+    every shot through NumPy's order, as osd_perms computes it."""
     import torch
     staged = []
     for slot, (H, syn, res) in enumerate(items):
@@ -225,36 +234,63 @@ def osd_device_stage(items, stream=None, slot0=0):
         if k == 0:
             staged.append(None)
             continue
-        host = _pinned(("post", slot0 + slot), (k, res.post.shape[1]), torch.float64)
-        host.copy_(res.post.index_select(0, bad), non_blocking=True)
+        n = res.post.shape[1]
+        code = _lib.code_for(H, dev.index)
+        post_b = res.post.index_select(0, bad)
+        syn_b = syn.index_select(0, bad)
+        e_b = res.ehat.index_select(0, bad)
+        status = torch.empty(k, dtype=torch.int32, device=dev)
+        cs = torch.cuda.current_stream(dev)
+        st = stream if stream is not None else cs.cuda_stream
+        status_h = _pinned(("status", slot0 + slot), (k,), torch.int32)
+        if n <= 2048 and not _host_order_only():
+            perm = torch.empty((k, n), dtype=torch.int32, device=dev)
+            tie = torch.empty(k, dtype=torch.int32, device=dev)
+            _lib.check(_lib.lib.qldpc_osd_device_ordered(code.handle, k, syn_b.data_ptr(), post_b.data_ptr(),
+                                                         int(order), e_b.data_ptr(), status.data_ptr(),
+                                                         perm.data_ptr(), tie.data_ptr(), st))
+        else:
+            status.fill_(2)                            # every shot takes NumPy's order
+        status_h.copy_(status, non_blocking=True)
         ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(dev))
-        staged.append((bad, host, ev, slot0 + slot))
+        ev.record(cs)
+        staged.append((bad, post_b, syn_b, e_b, status, status_h, ev, slot0 + slot))
     return staged
 
 
 def osd_device_finish(items, staged, order, stream=None):
-    """Second half: NumPy's reliability order on the host for each staged
-    decode (waiting only for its own copy), then the GPU elimination and the
-    scatter of the corrected estimates, all queued asynchronously."""
+    """Second half: for each staged decode (waiting only for its own event),
+    the shots the device order could not decide (status 2) get NumPy's
+    reliability order on the host (their posteriors only, pinned copies) and
+    the GPU elimination; then the corrected estimates are scattered back, all
+    queued asynchronously. res.osd_status keeps 0 / 1 per shot (1: the
+    reference's IndexError case, raised by osd_status_check)."""
     import torch
     for (H, syn, res), sg in zip(items, staged):
         if sg is None:
             continue
-        bad, host, ev, slot = sg
-        k = int(bad.numel())
+        bad, post_b, syn_b, e_b, status, status_h, ev, slot = sg
         dev = res.ehat.device
         code = _lib.code_for(H, dev.index)
         ev.synchronize()
-        perm_h = _pinned(("perm", slot), (k, host.shape[1]), torch.int32)
-        perm_h.numpy()[...] = osd_perms(host.numpy())
-        perms = perm_h.to(dev, non_blocking=True)
-        syn_b = syn.index_select(0, bad)
-        e_b = res.ehat.index_select(0, bad)
-        status = torch.empty(k, dtype=torch.int32, device=dev)
-        st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
-        _lib.check(_lib.lib.qldpc_osd_device(code.handle, k, syn_b.data_ptr(), perms.data_ptr(), int(order),
-                                             e_b.data_ptr(), status.data_ptr(), st))
+        redo = (status_h.numpy() == 2).nonzero()[0]
+        res.osd_host_order = int(redo.size)
+        if redo.size:
+            idx = torch.as_tensor(redo, device=dev)
+            k2 = int(redo.size)
+            host = _pinned(("post", slot), (k2, post_b.shape[1]), torch.float64)
+            host.copy_(post_b.index_select(0, idx))          # synchronous: needed right away
+            perm_h = _pinned(("perm", slot), (k2, post_b.shape[1]), torch.int32)
+            perm_h.numpy()[...] = osd_perms(host.numpy())
+            perms = perm_h.to(dev, non_blocking=True)
+            syn_r = syn_b.index_select(0, idx)
+            e_r = e_b.index_select(0, idx)
+            st2 = torch.empty(k2, dtype=torch.int32, device=dev)
+            st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+            _lib.check(_lib.lib.qldpc_osd_device(code.handle, k2, syn_r.data_ptr(), perms.data_ptr(), int(order),
+                                                 e_r.data_ptr(), st2.data_ptr(), st))
+            e_b.index_copy_(0, idx, e_r)
+            status.index_copy_(0, idx, st2)
         res.ehat.index_copy_(0, bad, e_b)
         res.osd_status = status      # checked by the caller (raises IndexError like the reference)
     return staged

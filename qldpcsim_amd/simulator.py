@@ -287,7 +287,7 @@ def simulate_p(Hx: np.ndarray, Hz: np.ndarray, p: float, shots: int = 1000, decT
                 ch.count_device(sy_z_, sy_x_, errX_, errZ_, rX_.ehat, rZ_.ehat, rX_.iters, rZ_.iters, acc)
             if cur is not None and osd >= 0:
                 cur[6] = decoders.osd_device_stage([(Hz, cur[0], cur[4]), (Hx, cur[1], cur[5])],
-                                                   slot0=2 * phase)
+                                                   slot0=2 * phase, order=osd)
                 phase ^= 1
             pending = cur
             if verbose and rank == 0 and cur is not None:

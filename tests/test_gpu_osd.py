@@ -78,3 +78,86 @@ def test_gpu_osd_index_error_case():
     from qldpcsim_amd import decoders
     with pytest.raises(IndexError):
         decoders.OSDdec(H, np.zeros(4, np.int8), np.array([1, 1]), np.array([0.1, 5.0, 6.0, 7.0]), 0)
+
+
+def _device_order(H, post):
+    import torch
+    from qldpcsim_amd import _lib
+    code = _lib.code_for(H, 0)
+    k, n = post.shape
+    p = torch.as_tensor(np.ascontiguousarray(post, np.float64), device="cuda")
+    perm = torch.empty((k, n), dtype=torch.int32, device="cuda")
+    tie = torch.empty(k, dtype=torch.int32, device="cuda")
+    _lib.check(_lib.lib.qldpc_osd_order_device(code.handle, k, p.data_ptr(), perm.data_ptr(), tie.data_ptr(), None))
+    torch.cuda.synchronize()
+    return perm.cpu().numpy(), tie.cpu().numpy()
+
+
+def _decoded_posteriors(code, p, shots, it, seed):
+    """Posteriors of non-converged layered MS decodes (the shots OSD sees)."""
+    from oracle import oracle
+    from qldpcsim_amd import codes, schedule, simulator
+    Hx, Hz = codes.load_code(code)
+    lx, _ = schedule.select_layers(Hx, Hz, "L")
+    lp, lr = schedule.pack_layers(lx, Hz.shape[0])
+    syn = simulator.sample_channel(Hx, Hz, p, shots, np.random.default_rng(seed))[0]
+    e, iters, post, _ = oracle.decode_batch("MS", Hz, syn, p / 3, it, lp, lr)
+    bad = np.any(((e.astype(np.int64) @ Hz.T.astype(np.int64)) % 2) != syn, axis=1)
+    return Hz, syn[bad], e[bad], post[bad]
+
+
+@pytest.mark.parametrize("code,p", [("LP118_2", 0.1), ("LP118_0", 0.08), ("LP04_0", 0.12)])
+def test_device_order_equals_numpy_below_tiepos(code, p):
+    """qldpc_osd_order_device: every sorted position below tiepos holds the
+    variable NumPy's argsort puts there (decoders.py:320-325), on posteriors
+    of real non-converged decodes and on random / tie-heavy rows."""
+    from qldpcsim_amd import decoders
+    H, syn, e, post = _decoded_posteriors(code, p, 600, 30, 7)
+    rng = np.random.default_rng(2)
+    extra = rng.normal(0, 4, (64, H.shape[1]))
+    extra[:16, ::3] = 2.5                                   # exact ties
+    extra[16:32] = np.round(extra[16:32] * 4) / 4            # many ties
+    extra[32:40, :7] = [150, -150, 99.5, -99.5, 37.0, -40.0, 0.0]   # clipped / saturated keys
+    post = np.concatenate([post, extra])
+    perm, tie = _device_order(H, post)
+    want = decoders.osd_perms(post)
+    n = H.shape[1]
+    assert np.all((tie >= 0) & (tie <= n))
+    for r in range(len(post)):
+        np.testing.assert_array_equal(perm[r, :tie[r]], want[r, :tie[r]], err_msg=f"row {r}")
+        assert sorted(perm[r]) == list(range(n))
+    assert (tie[-64:-48] < n).all()                          # exact ties are never certified
+    assert (tie[:-64] == n).mean() > 0.3                      # most decoded rows fully certified
+
+
+@pytest.mark.parametrize("code,p,order", [("LP118_2", 0.1, 0), ("LP118_0", 0.08, 1), ("LP04_0", 0.12, 4)])
+def test_ordered_device_osd_equals_numpy_ordered_osd(code, p, order):
+    """qldpc_osd_device_ordered gives the NumPy-ordered result on every shot it
+    decides (status 0) and leaves the rest untouched (status 2); the
+    apply_osd_device path (device order + host fallback) equals the host OSD
+    with NumPy's order on every shot."""
+    import torch
+    from qldpcsim_amd import _lib, decoders
+    H, syn, e, post = _decoded_posteriors(code, p, 800, 30, 9)
+    k = len(syn)
+    code_h = _lib.code_for(H, 0)
+    d = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a, dt), device="cuda")  # noqa: E731
+    s_d, p_d, e_d = d(syn, np.uint8), d(post, np.float64), d(e, np.uint8)
+    st = torch.empty(k, dtype=torch.int32, device="cuda")
+    perm = torch.empty((k, H.shape[1]), dtype=torch.int32, device="cuda")
+    tie = torch.empty(k, dtype=torch.int32, device="cuda")
+    _lib.check(_lib.lib.qldpc_osd_device_ordered(code_h.handle, k, s_d.data_ptr(), p_d.data_ptr(), order,
+                                                 e_d.data_ptr(), st.data_ptr(), perm.data_ptr(), tie.data_ptr(),
+                                                 None))
+    got, status = e_d.cpu().numpy(), st.cpu().numpy()
+    want, wst = _gpu_osd(H, syn, e, post, order)
+    assert np.all(wst == 0) and set(np.unique(status)) <= {0, 2}
+    ok = status == 0
+    np.testing.assert_array_equal(got[ok], want[ok])
+    np.testing.assert_array_equal(got[~ok], e[~ok])
+    assert ok.mean() > 0.5, ok.mean()
+    # the full device path with the host fallback
+    res = decoders.DecodeResult(d(e, np.uint8), torch.zeros(k, dtype=torch.int32, device="cuda"), p_d,
+                                torch.zeros(k, dtype=torch.int32, device="cuda"))
+    decoders.apply_osd_device(H, s_d, res, order)
+    np.testing.assert_array_equal(res.ehat.cpu().numpy(), want)

@@ -45,3 +45,17 @@ def test_fast_reliability_is_bit_identical():
     np.divide(1.0, t, out=t)
     np.maximum(t, np.subtract(1.0, t), out=t)
     np.testing.assert_array_equal(t.view(np.uint64), _literal_rel(P).view(np.uint64))
+
+
+def test_numpy_exp_within_one_ulp_on_the_reliability_domain():
+    """The device reliability order (qldpc_osd_order_device) certifies NumPy's
+    order where adjacent keys differ by more than 64 units in the last place;
+    that margin assumes NumPy's exp is within a few ulp of the true value on
+    [-100, 100]. Checked here against long-double exp."""
+    rng = np.random.default_rng(0)
+    x = np.concatenate([rng.uniform(-100, 100, 400000), rng.uniform(-1, 1, 100000)])
+    got = np.exp(x)
+    ref = np.exp(x.astype(np.longdouble))
+    ulp = np.spacing(got)
+    err = np.abs((got.astype(np.longdouble) - ref) / ulp.astype(np.longdouble))
+    assert float(err.max()) <= 1.0

@@ -44,6 +44,7 @@ for rep in range(3):
         t = tick("osd_count", t)
         decoders.apply_osd_device_many([(Hz, sy_z, rX), (Hx, sy_x, rZ)], osd)
         t = tick("osd", t)
+        T["osd_host_order_shots"] = T.get("osd_host_order_shots", 0) + rX.osd_host_order + rZ.osd_host_order
     c = ch.count(sy_z, sy_x, errX, errZ, rX.ehat, rZ.ehat, rX.iters, rZ.iters)
     t = tick("count", t)
 T = {k: (v / 2 if k != "osd_shots" else v / 2) for k, v in T.items()}
