@@ -68,6 +68,8 @@ def parse(argv=None):
                     help="depolarizing p for channel syndromes (device sampler); default: "
                          "uniform random syndromes (fixed work)")
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--io", default="bits", choices=["bits", "bytes"],
+                    help="syndrome / hard-decision format in HBM: bit-packed 64-bit words (default) or bytes")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="bounded CPU-baseline sample per leg (0 disables)")
     ap.add_argument("--worklog", default=None,
@@ -299,11 +301,15 @@ def run_rank(args, rank, world, local):
         ch = DeviceChannel(Hx, Hz, dev, seed=20251226 + rank)
         syn_z, syn_x, _, _ = ch.sample(args.p, B)
         prior = args.p / 3
+    bits = args.io == "bits"
+    if bits:                                             # the wire format of SURVEY 8f-4
+        syn_z, syn_x = decoders.pack_bits(syn_z), decoders.pack_bits(syn_x)
     halves = ((Hz, syn_z, lpx, lrx), (Hx, syn_x, lpz, lrz))
     want_post = False
 
     def buffers(H):
-        return decoders.DecodeResult(torch.empty((B, H.shape[1]), dtype=torch.uint8, device=dev),
+        eshape = (B, (H.shape[1] + 63) // 64) if bits else (B, H.shape[1])
+        return decoders.DecodeResult(torch.empty(eshape, dtype=torch.int64 if bits else torch.uint8, device=dev),
                                      torch.empty(B, dtype=torch.int32, device=dev), None,
                                      torch.empty(B, dtype=torch.int32, device=dev))
     outs = [buffers(H) for H, _, _, _ in halves]
@@ -315,7 +321,7 @@ def run_rank(args, rank, world, local):
         res = []
         for (H, s, lp, lr), o, nm in zip(halves, outs, names):
             r = decoders.decode_batch(H, s, prior, args.iters, algo=args.algo, out=o, layer_ptr=lp,
-                                      layer_rows=lr, want_post=want_post)
+                                      layer_rows=lr, want_post=want_post, ehat_bits=bits)
             res.append(r)
             if args.worklog:
                 log.append((nm, B, r.iters.sum(dtype=torch.int64)))
@@ -363,7 +369,8 @@ def run_rank(args, rank, world, local):
     it_per_launch = its / launches
     word = 4 if args.algo == "MS" else 8
     algo_bytes = sum(algorithmic_bytes_per_iter(H.astype(np.int64), lp, lr, word) for H, _, lp, lr in halves) / 2
-    algo_launch = algo_bytes * it_per_launch + (m + n + 4) * hs_per_launch
+    io_bytes = 8 * ((m + 63) // 64 + (n + 63) // 64) + 4 if bits else m + n + 4
+    algo_launch = algo_bytes * it_per_launch + io_bytes * hs_per_launch
     roof = roofline(names, avg_launch_s, hs_per_launch, it_per_launch, algo_launch, launches)
 
     sched_name = {"F": "flooding", "L": "layered", "S": "serial"}[args.schedule]
@@ -390,6 +397,7 @@ def run_rank(args, rank, world, local):
             "m": m, "n": n, "edges": E,
             "shots_per_gpu_per_step": B, "global_batch": B * world,
             "avg_iterations": its / halves_timed,
+            "io": "syndromes and hard decisions bit-packed (64-bit words)" if bits else "one byte per bit",
             "parallelism": f"shots sharded over {world} GPU(s) (one process per GPU, {backend}), "
                            "no data-path collective",
         },
@@ -417,7 +425,8 @@ def roofline(names, t_launch, hs_launch, it_launch, algo_launch, launches):
                  "algorithmic_gbs": algo_launch / t_launch / 1e9,
                  "algorithmic_model": "SURVEY.md 8d: per executed half-shot iteration w(3E+2n) flooding "
                                       "(layered: sum_l w(2E_l + sum_{V_l} d_j + 2|V_l|)), w = 4 MS / 8 BP, "
-                                      "+ m+n+4 I/O bytes per half-shot; an HBM-streaming design's bytes, "
+                                      "+ I/O bytes per half-shot (m+n+4, or 8(ceil(m/64)+ceil(n/64))+4 bit-packed); "
+                                      "an HBM-streaming design's bytes, "
                                       "not what this LDS-resident kernel moves",
                  "peak_gbs": HBM_PEAK_GBS},
          "device_code_sha256": sha, "profile": src}

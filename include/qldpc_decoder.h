@@ -44,6 +44,13 @@ extern "C" {
 #define QLDPC_ALGO_MS 0   /* normalized min-sum, decoders.py:110-182 */
 #define QLDPC_ALGO_BP 1   /* sum-product (tanh rule), decoders.py:189-290 */
 
+/* Bit formats of syndromes and hard decisions on the device (the *_ex entry
+ * points): one byte per bit, or 64-bit words with bit j % 64 of word j / 64
+ * (rows of ceil(len / 64) words; the layout of the sampler's error vectors,
+ * the reference's sample row bits packed, simulator.py:246-252). */
+#define QLDPC_FMT_BYTES 0
+#define QLDPC_FMT_BITS 1
+
 /* per-shot flag bits written to d_flags */
 #define QLDPC_FLAG_CONVERGED 1 /* a syndrome check passed (decoders.py:175-176 / :283-285) */
 #define QLDPC_FLAG_MIN_ZERO 2  /* MS: a check saw min|v|==0 (not emulated) */
@@ -101,7 +108,18 @@ int qldpc_decode_device(const qldpc_code *code, const qldpc_schedule *sched, int
 int qldpc_decode_kernel_name(const qldpc_code *code, const qldpc_schedule *sched, int algo,
                              char *buf, int len);
 
-/* Same with host buffers: stages through device memory, synchronous.
+/* qldpc_decode_device with a choice of formats: d_syn uint8 [batch][m]
+ * (QLDPC_FMT_BYTES) or uint64 [batch][ceil(m/64)] (QLDPC_FMT_BITS); d_ehat
+ * uint8 [batch][n] or uint64 [batch][ceil(n/64)]. Bit-packed I/O cuts the
+ * kernel's HBM bytes per half-shot from m + n to 8 (ceil(m/64) + ceil(n/64)). */
+int qldpc_decode_device_ex(const qldpc_code *code, const qldpc_schedule *sched, int algo, const void *d_syn,
+                           int syn_format, int64_t batch, double p, int max_iter, double beta, double eps,
+                           void *d_ehat, int ehat_format, int32_t *d_iters, double *d_post, int32_t *d_flags,
+                           void *stream);
+
+/* Same with host buffers: stages through page-locked host memory and device
+ * memory on a stream of its own (asynchronous DMA copies, then a wait on that
+ * stream only).
  * This is what the single-shot drop-in shims (MS_decoder / BP_decoder) use. */
 int qldpc_decode_host(const qldpc_code *code, const qldpc_schedule *sched, int algo,
                       const uint8_t *h_syn, int64_t batch, double p, int max_iter, double beta,
@@ -192,6 +210,16 @@ int qldpc_cpython_setdiff_first(int n, const int32_t *J, int nJ);
  * decode of Hz / sy_z); d_ehat_z: estimate of errZ (Hx / sy_x); d_iters_*
  * int32 [batch]. Asynchronous on `stream`, no host synchronisation. */
 int qldpc_channel_thresholds(double p, uint64_t *t1, uint64_t *t2, uint64_t *t3);
+/* _ex forms: syndromes (and, for the counters, estimates) in either
+ * QLDPC_FMT_* format. */
+int qldpc_channel_sample_ex(const qldpc_code *hx, const qldpc_code *hz, double p, uint64_t seed,
+                            uint64_t shot0, int64_t batch, uint64_t *d_errx, uint64_t *d_errz,
+                            void *d_syn_z, void *d_syn_x, int syn_format, void *stream);
+int qldpc_count_outcomes_ex(const qldpc_code *hx, const qldpc_code *hz, int64_t batch,
+                            const uint64_t *d_errx, const uint64_t *d_errz, const void *d_syn_z,
+                            const void *d_syn_x, int syn_format, const void *d_ehat_x, const void *d_ehat_z,
+                            int ehat_format, const int32_t *d_iters_x, const int32_t *d_iters_z,
+                            int64_t *d_counters, void *stream);
 int qldpc_channel_sample(const qldpc_code *hx, const qldpc_code *hz, double p, uint64_t seed,
                          uint64_t shot0, int64_t batch, uint64_t *d_errx, uint64_t *d_errz,
                          uint8_t *d_syn_z, uint8_t *d_syn_x, void *stream);

@@ -16,16 +16,18 @@ LIB_PATH = os.environ.get("QLDPC_LIB", os.path.join(_HERE, "_build", "libqldpc_h
 QLDPC_OK, QLDPC_EINVAL, QLDPC_ERANGE, QLDPC_EUNSUP, QLDPC_EHIP, QLDPC_ENOMEM = 0, -1, -2, -3, -4, -5
 ALGO = {"MS": 0, "BP": 1}
 FLAG_CONVERGED, FLAG_MIN_ZERO, FLAG_NONFINITE = 1, 2, 4
+FMT_BYTES, FMT_BITS = 0, 1          # syndrome / estimate formats (QLDPC_FMT_*)
 
 # every symbol include/qldpc_decoder.h declares
 EXPORTS = (
     "qldpc_last_error", "qldpc_version", "qldpc_device_count",
     "qldpc_code_create", "qldpc_code_destroy", "qldpc_code_shape",
     "qldpc_schedule_create", "qldpc_schedule_destroy",
-    "qldpc_decode_device", "qldpc_decode_host", "qldpc_decode_kernel_name",
+    "qldpc_decode_device", "qldpc_decode_device_ex", "qldpc_decode_host", "qldpc_decode_kernel_name",
     "qldpc_osd_decode", "qldpc_osd_decode_batch", "qldpc_osd_device", "qldpc_osd_order_device",
     "qldpc_osd_device_ordered", "qldpc_cpython_setdiff_first",
-    "qldpc_channel_thresholds", "qldpc_channel_sample", "qldpc_count_outcomes",
+    "qldpc_channel_thresholds", "qldpc_channel_sample", "qldpc_channel_sample_ex", "qldpc_count_outcomes",
+    "qldpc_count_outcomes_ex",
     "qldpc_timing_enable", "qldpc_timing_reset", "qldpc_timing_read",
 )
 
@@ -61,6 +63,7 @@ def _load():
         "qldpc_schedule_create": ([P, I, P, P, PP], I),
         "qldpc_schedule_destroy": ([P], I),
         "qldpc_decode_device": ([P, P, I, P, I64, D, I, D, D, P, P, P, P, P], I),
+        "qldpc_decode_device_ex": ([P, P, I, P, I, I64, D, I, D, D, P, I, P, P, P, P], I),
         "qldpc_decode_host": ([P, P, I, P, I64, D, I, D, D, P, P, P, P], I),
         "qldpc_decode_kernel_name": ([P, P, I, ctypes.c_char_p, I], I),
         "qldpc_osd_decode": ([P, P, P, I, P, P, P, I], I),
@@ -71,7 +74,9 @@ def _load():
         "qldpc_cpython_setdiff_first": ([I, P, I], I),
         "qldpc_channel_thresholds": ([D, P, P, P], I),
         "qldpc_channel_sample": ([P, P, D, ctypes.c_uint64, ctypes.c_uint64, I64, P, P, P, P, P], I),
+        "qldpc_channel_sample_ex": ([P, P, D, ctypes.c_uint64, ctypes.c_uint64, I64, P, P, P, P, I, P], I),
         "qldpc_count_outcomes": ([P, P, I64, P, P, P, P, P, P, P, P, P, P], I),
+        "qldpc_count_outcomes_ex": ([P, P, I64, P, P, P, P, I, P, P, I, P, P, P, P], I),
         "qldpc_timing_enable": ([I], I),
         "qldpc_timing_reset": ([], I),
         "qldpc_timing_read": ([P, P], I),

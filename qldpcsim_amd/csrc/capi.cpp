@@ -83,12 +83,17 @@ struct qldpc_code {
   std::vector<uint32_t> wc, avar;
   uint32_t filt_all = 0;
   uint32_t *d_wc = nullptr, *d_rtab = nullptr;  // rtab: [m][8] relabeled variables per row
-  // host staging workspace for qldpc_decode_host
+  // host staging workspace for qldpc_decode_host: device buffers, page-locked
+  // host mirrors (DMA copies) and a stream of its own (no device-wide sync)
   std::mutex ws_mu;
   int64_t ws_cap = 0;
   uint8_t *ws_syn = nullptr, *ws_ehat = nullptr;
   int32_t *ws_iters = nullptr, *ws_flags = nullptr;
   double* ws_post = nullptr;
+  uint8_t *hp_syn = nullptr, *hp_ehat = nullptr;
+  int32_t *hp_iters = nullptr, *hp_flags = nullptr;
+  double* hp_post = nullptr;
+  hipStream_t ws_stream = nullptr;
 };
 
 static int gf2_rank_cols(const std::vector<uint64_t>& cols, int n, int mw);
@@ -195,9 +200,14 @@ static void ws_free(qldpc_code* c) {
   (void)hipFree(c->ws_iters);
   (void)hipFree(c->ws_flags);
   (void)hipFree(c->ws_post);
-  c->ws_syn = c->ws_ehat = nullptr;
-  c->ws_iters = c->ws_flags = nullptr;
-  c->ws_post = nullptr;
+  (void)hipHostFree(c->hp_syn);
+  (void)hipHostFree(c->hp_ehat);
+  (void)hipHostFree(c->hp_iters);
+  (void)hipHostFree(c->hp_flags);
+  (void)hipHostFree(c->hp_post);
+  c->ws_syn = c->ws_ehat = c->hp_syn = c->hp_ehat = nullptr;
+  c->ws_iters = c->ws_flags = c->hp_iters = c->hp_flags = nullptr;
+  c->ws_post = c->hp_post = nullptr;
   c->ws_cap = 0;
 }
 
@@ -209,6 +219,7 @@ extern "C" int qldpc_code_destroy(qldpc_code* code) {
   (void)hipFree(code->d_wc);
   (void)hipFree(code->d_rtab);
   ws_free(code);
+  if (code->ws_stream) (void)hipStreamDestroy(code->ws_stream);
   delete code;
   return QLDPC_OK;
 }
@@ -688,7 +699,18 @@ extern "C" int qldpc_decode_device(const qldpc_code* code, const qldpc_schedule*
                                    const uint8_t* d_syn, int64_t batch, double p, int max_iter,
                                    double beta, double eps, uint8_t* d_ehat, int32_t* d_iters,
                                    double* d_post, int32_t* d_flags, void* stream) {
+  return qldpc_decode_device_ex(code, sched_c, algo, d_syn, QLDPC_FMT_BYTES, batch, p, max_iter, beta, eps, d_ehat,
+                                QLDPC_FMT_BYTES, d_iters, d_post, d_flags, stream);
+}
+
+extern "C" int qldpc_decode_device_ex(const qldpc_code* code, const qldpc_schedule* sched_c, int algo,
+                                      const void* d_syn, int syn_format, int64_t batch, double p, int max_iter,
+                                      double beta, double eps, void* d_ehat, int ehat_format, int32_t* d_iters,
+                                      double* d_post, int32_t* d_flags, void* stream) {
   auto* sched = const_cast<qldpc_schedule*>(sched_c);
+  if ((syn_format != QLDPC_FMT_BYTES && syn_format != QLDPC_FMT_BITS) ||
+      (ehat_format != QLDPC_FMT_BYTES && ehat_format != QLDPC_FMT_BITS))
+    return fail(QLDPC_EINVAL, "unknown syndrome / estimate format");
   if (!code || !sched) return fail(QLDPC_EINVAL, "code/schedule is null");
   if (sched->code != code) return fail(QLDPC_EINVAL, "schedule was built for a different code");
   if (algo != QLDPC_ALGO_MS && algo != QLDPC_ALGO_BP) return fail(QLDPC_EINVAL, "Unrecognized decoder type.");
@@ -707,6 +729,8 @@ extern "C" int qldpc_decode_device(const qldpc_code* code, const qldpc_schedule*
   LaunchCfg* cfg = nullptr;
   int rc = launch_config(sched, algo, &cfg);
   if (rc) return rc;
+  if (ehat_format == QLDPC_FMT_BITS && cfg->slice)
+    return fail(QLDPC_EUNSUP, "bit-packed estimates are not written by ms_layered_grp_kernel (unset QLDPC_MS_GROUPS)");
 
   DecodeArgs a{};
   a.blob = sched->d_blob;
@@ -745,8 +769,12 @@ extern "C" int qldpc_decode_device(const qldpc_code* code, const qldpc_schedule*
   a.E = code->E;
   a.n_layers = sched->n_layers;
   a.vinv = code->d_vinv;
-  a.syn = d_syn;
-  a.ehat = d_ehat;
+  a.syn = (const uint8_t*)d_syn;
+  a.ehat = (uint8_t*)d_ehat;
+  a.syn_bits = syn_format == QLDPC_FMT_BITS;
+  a.eh_bits = ehat_format == QLDPC_FMT_BITS;
+  a.wm = (code->m + 63) / 64;
+  a.wn = (code->n + 63) / 64;
   a.iters = d_iters;
   a.post = d_post;
   a.flags = d_flags;
@@ -827,6 +855,7 @@ extern "C" int qldpc_decode_host(const qldpc_code* code_c, const qldpc_schedule*
   if (code->device < 0) return fail(QLDPC_EHIP, "no HIP device was visible when the code was created");
   std::lock_guard<std::mutex> lk(code->ws_mu);
   const int m = code->m, n = code->n;
+  if (!code->ws_stream) HIP_TRY(hipStreamCreateWithFlags(&code->ws_stream, hipStreamNonBlocking));
   if (batch > code->ws_cap) {
     ws_free(code);
     const int64_t cap = std::max<int64_t>(batch, 64);
@@ -835,20 +864,32 @@ extern "C" int qldpc_decode_host(const qldpc_code* code_c, const qldpc_schedule*
     HIP_TRY(hipMalloc(&code->ws_iters, sizeof(int32_t) * cap));
     HIP_TRY(hipMalloc(&code->ws_flags, sizeof(int32_t) * cap));
     HIP_TRY(hipMalloc(&code->ws_post, sizeof(double) * std::max<int64_t>(1, cap * n)));
+    HIP_TRY(hipHostMalloc(&code->hp_syn, std::max<int64_t>(1, cap * m)));
+    HIP_TRY(hipHostMalloc(&code->hp_ehat, std::max<int64_t>(1, cap * n)));
+    HIP_TRY(hipHostMalloc(&code->hp_iters, sizeof(int32_t) * cap));
+    HIP_TRY(hipHostMalloc(&code->hp_flags, sizeof(int32_t) * cap));
+    HIP_TRY(hipHostMalloc(&code->hp_post, sizeof(double) * std::max<int64_t>(1, cap * n)));
     code->ws_cap = cap;
   }
-  if (batch * m) HIP_TRY(hipMemcpy(code->ws_syn, h_syn, batch * m, hipMemcpyHostToDevice));
+  hipStream_t st = code->ws_stream;
+  if (batch * m) {
+    memcpy(code->hp_syn, h_syn, batch * m);
+    HIP_TRY(hipMemcpyAsync(code->ws_syn, code->hp_syn, batch * m, hipMemcpyHostToDevice, st));
+  }
   int rc = qldpc_decode_device(code, sched, algo, code->ws_syn, batch, p, max_iter, beta, eps,
                                code->ws_ehat, code->ws_iters, h_post ? code->ws_post : nullptr,
-                               code->ws_flags, nullptr);
+                               code->ws_flags, st);
   if (rc) return rc;
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipDeviceSynchronize());
-  if (batch * n) HIP_TRY(hipMemcpy(h_ehat, code->ws_ehat, batch * n, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(h_iters, code->ws_iters, sizeof(int32_t) * batch, hipMemcpyDeviceToHost));
-  if (h_flags) HIP_TRY(hipMemcpy(h_flags, code->ws_flags, sizeof(int32_t) * batch, hipMemcpyDeviceToHost));
+  if (batch * n) HIP_TRY(hipMemcpyAsync(code->hp_ehat, code->ws_ehat, batch * n, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(code->hp_iters, code->ws_iters, sizeof(int32_t) * batch, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(code->hp_flags, code->ws_flags, sizeof(int32_t) * batch, hipMemcpyDeviceToHost, st));
   if (h_post && batch * n)
-    HIP_TRY(hipMemcpy(h_post, code->ws_post, sizeof(double) * batch * n, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpyAsync(code->hp_post, code->ws_post, sizeof(double) * batch * n, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));                  // this stream only
+  if (batch * n) memcpy(h_ehat, code->hp_ehat, batch * n);
+  memcpy(h_iters, code->hp_iters, sizeof(int32_t) * batch);
+  if (h_flags) memcpy(h_flags, code->hp_flags, sizeof(int32_t) * batch);
+  if (h_post && batch * n) memcpy(h_post, code->hp_post, sizeof(double) * batch * n);
   return QLDPC_OK;
 }
 
@@ -1269,6 +1310,14 @@ extern "C" int qldpc_channel_thresholds(double p, uint64_t* t1, uint64_t* t2, ui
 extern "C" int qldpc_channel_sample(const qldpc_code* hx, const qldpc_code* hz, double p, uint64_t seed,
                                     uint64_t shot0, int64_t batch, uint64_t* d_errx, uint64_t* d_errz,
                                     uint8_t* d_syn_z, uint8_t* d_syn_x, void* stream) {
+  return qldpc_channel_sample_ex(hx, hz, p, seed, shot0, batch, d_errx, d_errz, d_syn_z, d_syn_x,
+                                 QLDPC_FMT_BYTES, stream);
+}
+
+extern "C" int qldpc_channel_sample_ex(const qldpc_code* hx, const qldpc_code* hz, double p, uint64_t seed,
+                                       uint64_t shot0, int64_t batch, uint64_t* d_errx, uint64_t* d_errz,
+                                       void* d_syn_z, void* d_syn_x, int syn_format, void* stream) {
+  if (syn_format != QLDPC_FMT_BYTES && syn_format != QLDPC_FMT_BITS) return fail(QLDPC_EINVAL, "unknown syndrome format");
   qldpc::SampleArgs a{};
   int rc = pair_tabs(hx, hz, &a.t);
   if (rc != QLDPC_OK) return rc;
@@ -1280,8 +1329,9 @@ extern "C" int qldpc_channel_sample(const qldpc_code* hx, const qldpc_code* hz, 
     return fail(QLDPC_EINVAL, "null device buffer");
   a.errx = d_errx;
   a.errz = d_errz;
-  a.syz = d_syn_z;
-  a.syx = d_syn_x;
+  a.syz = (uint8_t*)d_syn_z;
+  a.syx = (uint8_t*)d_syn_x;
+  a.syn_bits = syn_format == QLDPC_FMT_BITS;
   a.batch = batch;
   a.shot0 = shot0;
   a.key0 = (uint32_t)seed;
@@ -1295,6 +1345,18 @@ extern "C" int qldpc_count_outcomes(const qldpc_code* hx, const qldpc_code* hz, 
                                     const uint8_t* d_syn_x, const uint8_t* d_ehat_x, const uint8_t* d_ehat_z,
                                     const int32_t* d_iters_x, const int32_t* d_iters_z, int64_t* d_counters,
                                     void* stream) {
+  return qldpc_count_outcomes_ex(hx, hz, batch, d_errx, d_errz, d_syn_z, d_syn_x, QLDPC_FMT_BYTES, d_ehat_x,
+                                 d_ehat_z, QLDPC_FMT_BYTES, d_iters_x, d_iters_z, d_counters, stream);
+}
+
+extern "C" int qldpc_count_outcomes_ex(const qldpc_code* hx, const qldpc_code* hz, int64_t batch,
+                                       const uint64_t* d_errx, const uint64_t* d_errz, const void* d_syn_z,
+                                       const void* d_syn_x, int syn_format, const void* d_ehat_x,
+                                       const void* d_ehat_z, int ehat_format, const int32_t* d_iters_x,
+                                       const int32_t* d_iters_z, int64_t* d_counters, void* stream) {
+  if ((syn_format != QLDPC_FMT_BYTES && syn_format != QLDPC_FMT_BITS) ||
+      (ehat_format != QLDPC_FMT_BYTES && ehat_format != QLDPC_FMT_BITS))
+    return fail(QLDPC_EINVAL, "unknown syndrome / estimate format");
   qldpc::CountArgs a{};
   int rc = pair_tabs(hx, hz, &a.t);
   if (rc != QLDPC_OK) return rc;
@@ -1305,10 +1367,12 @@ extern "C" int qldpc_count_outcomes(const qldpc_code* hx, const qldpc_code* hz, 
     return fail(QLDPC_EINVAL, "null device buffer");
   a.errx = d_errx;
   a.errz = d_errz;
-  a.syz = d_syn_z;
-  a.syx = d_syn_x;
-  a.ehx = d_ehat_x;
-  a.ehz = d_ehat_z;
+  a.syz = (const uint8_t*)d_syn_z;
+  a.syx = (const uint8_t*)d_syn_x;
+  a.ehx = (const uint8_t*)d_ehat_x;
+  a.ehz = (const uint8_t*)d_ehat_z;
+  a.syn_bits = syn_format == QLDPC_FMT_BITS;
+  a.eh_bits = ehat_format == QLDPC_FMT_BITS;
   a.itx = d_iters_x;
   a.itz = d_iters_z;
   a.acc = reinterpret_cast<unsigned long long*>(d_counters);

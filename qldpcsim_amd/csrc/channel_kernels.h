@@ -21,8 +21,9 @@ struct SampleArgs {
   PairTabs t;
   uint64_t* errx;  // [batch][W]
   uint64_t* errz;  // [batch][W]
-  uint8_t* syz;    // [batch][mz]  Hz errX mod 2
+  uint8_t* syz;    // [batch][mz]  Hz errX mod 2 (syn_bits: uint64 [batch][ceil(mz/64)])
   uint8_t* syx;    // [batch][mx]  Hx errZ mod 2
+  int syn_bits;
   long long batch;
   uint64_t shot0;
   uint32_t key0, key1;
@@ -37,6 +38,7 @@ struct CountArgs {
   const uint8_t* syx;    // [batch][mx]
   const uint8_t* ehx;    // [batch][n] X-half estimate (decodes Hz)
   const uint8_t* ehz;    // [batch][n] Z-half estimate (decodes Hx)
+  int syn_bits, eh_bits; // uint64 words instead of bytes (bit j % 64 of word j / 64)
   const int32_t* itx;    // [batch]
   const int32_t* itz;
   unsigned long long* acc;  // [6] accumulated

@@ -11,8 +11,9 @@
 //     X if u < T1, Y if T1 <= u < T2, Z if T2 <= u < T3, T_k = floor(k·(p/3)·2^32)
 //     errX = X | Y, errZ = Z | Y, sy_z = Hz·errX mod 2, sy_x = Hx·errZ mod 2
 // Error vectors are written bit-packed (bit j % 64 of word j / 64): they are
-// only read again by the counters. Syndromes are written as bytes, the
-// decoder's input format. oracle/qldpc_oracle.c restates the same stream.
+// only read again by the counters. Syndromes are written as bytes or, with
+// syn_bits, as words of the same layout (the decoder reads either).
+// oracle/qldpc_oracle.c restates the same stream.
 //
 // count_outcomes_kernel forms the reference's per-shot outcomes
 // (simulator.py:291-303) and sums them into six int64 counters:
@@ -146,10 +147,24 @@ __global__ void __launch_bounds__(64 * kChannelWaves) channel_sample_kernel(Samp
       a.errz[b * W + lane] = myz;
     }
     wave_sync();
-    for (int c = lane; c < t.mz; c += 64)
-      a.syz[b * t.mz + c] = (uint8_t)row_parity<DC>(tb.rpz, tb.ciz, c, wx32);
-    for (int c = lane; c < t.mx; c += 64)
-      a.syx[b * t.mx + c] = (uint8_t)row_parity<DC>(tb.rpx, tb.cix, c, wz32);
+    if (a.syn_bits) {                           // one 64-bit word per 64 checks (ballot)
+      const int wmz = (t.mz + 63) >> 6, wmx = (t.mx + 63) >> 6;
+      for (int c0 = 0; c0 < t.mz; c0 += 64) {
+        const int c = c0 + lane;
+        const uint64_t bits = __ballot(c < t.mz && row_parity<DC>(tb.rpz, tb.ciz, c < t.mz ? c : 0, wx32));
+        if (lane == 0) reinterpret_cast<uint64_t*>(a.syz)[b * wmz + (c0 >> 6)] = bits;
+      }
+      for (int c0 = 0; c0 < t.mx; c0 += 64) {
+        const int c = c0 + lane;
+        const uint64_t bits = __ballot(c < t.mx && row_parity<DC>(tb.rpx, tb.cix, c < t.mx ? c : 0, wz32));
+        if (lane == 0) reinterpret_cast<uint64_t*>(a.syx)[b * wmx + (c0 >> 6)] = bits;
+      }
+    } else {
+      for (int c = lane; c < t.mz; c += 64)
+        a.syz[b * t.mz + c] = (uint8_t)row_parity<DC>(tb.rpz, tb.ciz, c, wx32);
+      for (int c = lane; c < t.mx; c += 64)
+        a.syx[b * t.mx + c] = (uint8_t)row_parity<DC>(tb.rpx, tb.cix, c, wz32);
+    }
     wave_sync();  // the next shot overwrites wx / wz
   }
 }
@@ -216,8 +231,15 @@ __global__ void __launch_bounds__(64 * kChannelWaves) count_outcomes_kernel(Coun
     // this shot's true errors and iteration counts: loads in flight early
     const uint64_t tx = lane < W ? a.errx[b * W + lane] : 0, tz = lane < W ? a.errz[b * W + lane] : 0;
     const int itx = a.itx[b], itz = a.itz[b];
-    pack_estimate<VEC>(a.ehx + b * n, n, W, lane, reinterpret_cast<uint8_t*>(ex));
-    pack_estimate<VEC>(a.ehz + b * n, n, W, lane, reinterpret_cast<uint8_t*>(ez));
+    if (a.eh_bits) {                            // already words
+      if (lane < W) {
+        ex[lane] = reinterpret_cast<const uint64_t*>(a.ehx)[b * W + lane];
+        ez[lane] = reinterpret_cast<const uint64_t*>(a.ehz)[b * W + lane];
+      }
+    } else {
+      pack_estimate<VEC>(a.ehx + b * n, n, W, lane, reinterpret_cast<uint8_t*>(ex));
+      pack_estimate<VEC>(a.ehz + b * n, n, W, lane, reinterpret_cast<uint8_t*>(ez));
+    }
     wave_sync();
     bool lane_exact = true, lane_degen = true;
     if (lane < W) {
@@ -230,10 +252,17 @@ __global__ void __launch_bounds__(64 * kChannelWaves) count_outcomes_kernel(Coun
     bool fx = false, fz = false;
     const uint32_t* ex32 = reinterpret_cast<const uint32_t*>(ex);
     const uint32_t* ez32 = reinterpret_cast<const uint32_t*>(ez);
-    for (int c = lane; c < t.mz; c += 64)
-      fx |= row_parity<DC>(tb.rpz, tb.ciz, c, ex32) != a.syz[b * t.mz + c];
-    for (int c = lane; c < t.mx; c += 64)
-      fz |= row_parity<DC>(tb.rpx, tb.cix, c, ez32) != a.syx[b * t.mx + c];
+    const int wmz = (t.mz + 63) >> 6, wmx = (t.mx + 63) >> 6;
+    for (int c = lane; c < t.mz; c += 64) {
+      const uint32_t s = a.syn_bits ? (uint32_t)(reinterpret_cast<const uint64_t*>(a.syz)[b * wmz + (c >> 6)] >> (c & 63)) & 1u
+                                    : a.syz[b * t.mz + c];
+      fx |= row_parity<DC>(tb.rpz, tb.ciz, c, ex32) != s;
+    }
+    for (int c = lane; c < t.mx; c += 64) {
+      const uint32_t s = a.syn_bits ? (uint32_t)(reinterpret_cast<const uint64_t*>(a.syx)[b * wmx + (c >> 6)] >> (c & 63)) & 1u
+                                    : a.syx[b * t.mx + c];
+      fz |= row_parity<DC>(tb.rpx, tb.cix, c, ez32) != s;
+    }
     const bool failx = __ballot(fx) != 0, failz = __ballot(fz) != 0;
     if (lane == 0) {
       cnt[0] += failx;

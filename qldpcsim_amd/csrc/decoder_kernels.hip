@@ -90,6 +90,25 @@ __device__ __forceinline__ void store_bits64(uint32_t* words, int c0, int pred, 
   if (lane == 1) words[(c0 >> 5) + 1] = (uint32_t)(b >> 32);
 }
 
+// Bit-packed I/O (DecodeArgs::syn_bits / eh_bits): syndromes and hard
+// decisions as 64-bit words, bit j % 64 of word j / 64 (the error-vector
+// layout of the device sampler), instead of one byte per bit.
+__device__ __forceinline__ uint32_t syn_bit(const DecodeArgs& a, long long hs, int c) {
+  if (a.syn_bits) return (uint32_t)(((const uint64_t*)a.syn)[hs * a.wm + (c >> 6)] >> (c & 63)) & 1u;
+  return a.syn[hs * (long long)a.m + c] & 1u;
+}
+// ê_jo of half-shot hs. Callers visit columns in 64-aligned wave chunks
+// (lane l holds column 64 k + l), so with eh_bits the chunk is one ballot and
+// lane 0 stores the word.
+__device__ __forceinline__ void put_ehat(const DecodeArgs& a, long long hs, int jo, bool bit) {
+  if (a.eh_bits) {
+    const uint64_t b = ballot(bit);
+    if ((jo & 63) == 0) ((uint64_t*)a.ehat)[hs * a.wn + (jo >> 6)] = b;
+  } else {
+    a.ehat[hs * (long long)a.n + jo] = (uint8_t)bit;
+  }
+}
+
 // Half-shot prologue / epilogue with every global load issued up front (a
 // loop of dependent load -> use steps paid one HBM latency per 64 elements).
 // The relabeling vinv is per code, so it is read once per kernel into
@@ -114,7 +133,6 @@ template <int NJ>
 __device__ __forceinline__ void write_outputs(const DecodeArgs& a, const VinvRegs<NJ>& vr, const double* post,
                                               long long hs, int lane) {
   const int n = a.n;
-  uint8_t* eh = a.ehat + hs * (long long)n;
   double* po = a.post ? a.post + hs * (long long)n : nullptr;
   if (n <= 64 * NJ) {
 #pragma unroll
@@ -122,14 +140,14 @@ __device__ __forceinline__ void write_outputs(const DecodeArgs& a, const VinvReg
       const int jo = 64 * k + lane;
       if (64 * k < n && jo < n) {
         const double pv = post[vr.get(k)];
-        eh[jo] = (uint8_t)(pv < 0.0);
+        put_ehat(a, hs, jo, pv < 0.0);
         if (po) po[jo] = pv;
       }
     }
   } else {
     for (int jo = lane; jo < n; jo += 64) {
       const double pv = post[a.vinv[jo]];
-      eh[jo] = (uint8_t)(pv < 0.0);
+      put_ehat(a, hs, jo, pv < 0.0);
       if (po) po[jo] = pv;
     }
   }
@@ -138,7 +156,14 @@ __device__ __forceinline__ void write_outputs(const DecodeArgs& a, const VinvReg
 // syndrome bits of one half-shot into the per-wave word array (m <= 64 NC:
 // all byte loads in flight together; larger m loops)
 template <int NC>
-__device__ __forceinline__ void load_syndrome_bits(const uint8_t* syn, int m, uint32_t* synw, int lane) {
+__device__ __forceinline__ void load_syndrome_bits(const DecodeArgs& a, long long hs, uint32_t* synw, int lane) {
+  const int m = a.m;
+  if (a.syn_bits) {                                 // already words: copy them
+    const uint32_t* src = (const uint32_t*)((const uint64_t*)a.syn + hs * a.wm);
+    for (int w = lane; w < 2 * a.wm; w += 64) synw[w] = src[w];
+    return;
+  }
+  const uint8_t* syn = a.syn + hs * (long long)m;
   if (m <= 64 * NC) {
     uint32_t b[NC];
 #pragma unroll
@@ -650,7 +675,6 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) decode_kernel(DecodeArgs a)
   for (HalfShotQueue Q(a, waves, wid); Q.hs < a.batch; Q.advance()) {
     const long long hs = Q.hs;
     Q.prefetch(threadIdx.x & 63);
-    const uint8_t* syn = a.syn + hs * (long long)m;
     int fl = 0;
     int iters = a.max_iter;
     bool conv = false;
@@ -658,7 +682,7 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) decode_kernel(DecodeArgs a)
     if constexpr (!LAYERED) {
       // ---------------- flooding: one layer holding every check ------------
       uint32_t synreg = 0;  // bit i = syndrome of check lane + 64 i
-      for (int i = 0, c = lane; c < m; ++i, c += 64) synreg |= (uint32_t)(syn[c] & 1) << i;
+      for (int i = 0, c = lane; c < m; ++i, c += 64) synreg |= syn_bit(a, hs, c) << i;
       if constexpr (ALGO == ALGO_BP) {
         // BP's first check-node pass reads v2c = L0 (decoders.py:235):
         // post = L0, c2v = 0. (MS's first pass reads float32(L) directly.)
@@ -736,7 +760,7 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) decode_kernel(DecodeArgs a)
       for (int c0 = 0; c0 < m; c0 += 64) {
         const int c = c0 + lane;
         const int in = c < m;
-        store_bits64(synw, c0, in ? (syn[c] & 1) : 0, lane);
+        store_bits64(synw, c0, in ? (int)syn_bit(a, hs, c) : 0, lane);
         int deg = 0;
         if (in) deg = DC ? DC : (int)g.row_ptr[c + 1] - (int)g.row_ptr[c];
         store_bits64(parw, c0, in && (L < 0.0) && (deg & 1), lane);
@@ -785,11 +809,10 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) decode_kernel(DecodeArgs a)
     }
 
     // ---------------- outputs (original column order) ----------------------
-    uint8_t* eh = a.ehat + hs * (long long)n;
     double* po = a.post ? a.post + hs * (long long)n : nullptr;
     for (int jo = lane; jo < n; jo += 64) {
       const double pv = post[a.vinv[jo]];
-      eh[jo] = (uint8_t)(pv < 0.0);                  // e_hat = post < 0 (:174 / :280)
+      put_ehat(a, hs, jo, pv < 0.0);                  // e_hat = post < 0 (:174 / :280)
       if (po) po[jo] = pv;
     }
     // OR the lane-local flags across the wave
@@ -947,7 +970,6 @@ ms_flood_kernel(DecodeArgs a) {
   for (HalfShotQueue Q(a, waves, wid); Q.hs < a.batch; Q.advance()) {
     const long long hs = Q.hs;
     Q.prefetch(threadIdx.x & 63);
-    const uint8_t* syn = a.syn + hs * (long long)m;
     int fl = 0;
     int iters = a.max_iter;
     bool conv = false;
@@ -955,7 +977,7 @@ ms_flood_kernel(DecodeArgs a) {
 #pragma unroll
     for (int i = 0; i < KC; ++i) {
       const int c = lane + 64 * i;
-      if (c < m) synreg |= (uint32_t)(syn[c] & 1) << i;
+      if (c < m) synreg |= syn_bit(a, hs, c) << i;
     }
     for (int it = 0;; ++it) {
       uint32_t unsat = 0;
@@ -1023,11 +1045,10 @@ ms_flood_kernel(DecodeArgs a) {
         break;
       }
     }
-    uint8_t* eh = a.ehat + hs * (long long)n;
     double* po = a.post ? a.post + hs * (long long)n : nullptr;
     for (int jo = lane; jo < n; jo += 64) {
       const double pv = post[a.vinv[jo]];
-      eh[jo] = (uint8_t)(pv < 0.0);
+      put_ehat(a, hs, jo, pv < 0.0);
       if (po) po[jo] = pv;
     }
     const uint64_t b1 = ballot((fl & FLAG_MIN_ZERO) != 0);
@@ -1309,12 +1330,11 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
   for (HalfShotQueue Q(a, waves, wid); Q.hs < a.batch; Q.advance()) {
     const long long hs = Q.hs;
     Q.prefetch(threadIdx.x & 63);
-    const uint8_t* syn = a.syn + hs * (long long)m;
     int fl = 0;
     int iters = a.max_iter;
     bool conv = false;
     const double L = a.L;
-    load_syndrome_bits<8>(syn, m, synw, lane);
+    load_syndrome_bits<8>(a, hs, synw, lane);
     for (int j = lane; j < n; j += 64) colS[j] = 0.0f;          // post = L, c2v = 0 (:148-150)
     for (int p = lane; p < a.E; p += 64) c2v[p] = 0.0f;
     wave_sync();
@@ -1374,19 +1394,18 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
       }
     }
     {                                                          // ê, posteriors in original order
-      uint8_t* eh = a.ehat + hs * (long long)n;
       double* po = a.post ? a.post + hs * (long long)n : nullptr;
       for (int k = 0; k < 16 && 64 * k < n; ++k) {
         const int jo = 64 * k + lane;
         if (jo < n) {
           const double pv = L + (double)colS[n <= 1024 ? vr.get(k) : a.vinv[jo]];
-          eh[jo] = (uint8_t)(pv < 0.0);
+          put_ehat(a, hs, jo, pv < 0.0);
           if (po) po[jo] = pv;
         }
       }
       for (int jo = 1024 + lane; jo < n; jo += 64) {
         const double pv = L + (double)colS[a.vinv[jo]];
-        eh[jo] = (uint8_t)(pv < 0.0);
+        put_ehat(a, hs, jo, pv < 0.0);
         if (po) po[jo] = pv;
       }
     }
@@ -1555,8 +1574,7 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_grp_kernel(Decod
 
   // starts half-shot Q.hs in this group's slice (lanes of starting groups only)
   auto start = [&]() {
-    const uint8_t* syn = a.syn + Q.hs * (long long)m;
-    for (int c = sl; c < m; c += LPH) synb[c] = syn[c] & 1;
+    for (int c = sl; c < m; c += LPH) synb[c] = (uint8_t)syn_bit(a, Q.hs, c);
     for (int j = sl; j < n; j += LPH) colS[j] = 0.0f;            // post = L, c2v = 0 (:148-150)
     for (int p = sl; p < a.E; p += LPH) c2v[p] = 0.0f;
     lay = 0;
@@ -1648,11 +1666,10 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_grp_kernel(Decod
       if (done) {
         // ê and posteriors in original column order
         const long long hs = Q.hs;
-        uint8_t* eh = a.ehat + hs * (long long)n;
         double* po = a.post ? a.post + hs * (long long)n : nullptr;
         for (int jo = sl; jo < n; jo += LPH) {
           const double pv = L + (double)colS[a.vinv[jo]];
-          eh[jo] = (uint8_t)(pv < 0.0);
+          put_ehat(a, hs, jo, pv < 0.0);
           if (po) po[jo] = pv;
         }
         if (sl == 0) {
@@ -1796,7 +1813,6 @@ __global__ void __launch_bounds__(64 * W) bp_team_kernel(DecodeArgs a) {
       claimed = true;
       if (tid == 0) tk = atomicAdd(a.queue, tlen);
     }
-    const uint8_t* syn = a.syn + hs * (long long)m;
     int fl = 0;
     int iters = a.max_iter;
     bool conv = false;
@@ -1808,7 +1824,7 @@ __global__ void __launch_bounds__(64 * W) bp_team_kernel(DecodeArgs a) {
     for (int c0 = 64 * wid; c0 < m; c0 += TS) {
       const int c = c0 + lane;
       const int in = c < m;
-      store_bits64(synw, c0, in ? (syn[c] & 1) : 0, lane);
+      store_bits64(synw, c0, in ? (int)syn_bit(a, hs, c) : 0, lane);
       if constexpr (LAYERED) store_bits64(parw, c0, in && (L < 0.0) && (DC & 1), lane);
     }
     __syncthreads();
@@ -1881,12 +1897,10 @@ __global__ void __launch_bounds__(64 * W) bp_team_kernel(DecodeArgs a) {
         }
       }
     }
-
-    uint8_t* eh = a.ehat + hs * (long long)n;
     double* po = a.post ? a.post + hs * (long long)n : nullptr;
     for (int jo = tid; jo < n; jo += TS) {
       const double pv = post[a.vinv[jo]];
-      eh[jo] = (uint8_t)(pv < 0.0);                       // (:280)
+      put_ehat(a, hs, jo, pv < 0.0);                       // (:280)
       if (po) po[jo] = pv;
     }
     const bool nonfin = team_any((fl & FLAG_NONFINITE) != 0);

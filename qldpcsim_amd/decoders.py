@@ -31,7 +31,8 @@ import numpy as np
 from . import _lib
 from .schedule import pack_layers
 
-__all__ = ["MS_decoder", "BP_decoder", "OSDdec", "decode_batch", "DecodeResult", "osd_perm",
+__all__ = ["MS_decoder", "BP_decoder", "OSDdec", "decode_batch", "DecodeResult", "osd_perm", "pack_bits",
+           "unpack_bits",
            "osd_perms", "apply_osd", "apply_osd_device", "apply_osd_device_many", "osd_device_stage",
            "osd_device_finish", "osd_status_check"]
 
@@ -52,14 +53,36 @@ def _is_torch(x):
     return type(x).__module__.startswith("torch")
 
 
+def pack_bits(bits):
+    """uint8 [B, k] 0/1 tensor -> int64 [B, ceil(k/64)] words, bit j % 64 of
+    word j / 64 (the bit-packed syndrome / estimate format, QLDPC_FMT_BITS)."""
+    import torch
+    B, k = bits.shape
+    W = (k + 63) // 64
+    x = torch.zeros((B, 64 * W), dtype=torch.int64, device=bits.device)
+    x[:, :k] = bits.to(torch.int64) & 1
+    sh = torch.arange(64, device=bits.device, dtype=torch.int64)
+    return (x.view(B, W, 64) << sh).sum(dim=2)
+
+
+def unpack_bits(words, k):
+    """int64 [B, W] words -> uint8 [B, k] (inverse of pack_bits)."""
+    import torch
+    sh = torch.arange(64, device=words.device, dtype=torch.int64)
+    return ((words.unsqueeze(-1) >> sh) & 1).to(torch.uint8).reshape(words.shape[0], -1)[:, :k]
+
+
 def decode_batch(H, syndromes, p, max_iter, layers=None, algo="MS", beta=0.75, eps=1e-9,
                  want_post=False, osd_order=-1, layer_ptr=None, layer_rows=None, stream=None,
-                 out=None):
+                 out=None, ehat_bits=False):
     """Decode a batch of syndromes of one matrix on the GPU.
 
     syndromes: uint8 [B, m] NumPy array (host; staged, synchronous) or a
-    torch uint8 tensor on a HIP device (asynchronous on `stream` or torch's
-    current stream; outputs are device tensors, OSD is not applied).
+    torch tensor on a HIP device (asynchronous on `stream` or torch's current
+    stream; outputs are device tensors, OSD is not applied): uint8 [B, m] one
+    byte per check, or int64 [B, ceil(m/64)] bit-packed words (pack_bits).
+    `ehat_bits` (device path): hard decisions as int64 [B, ceil(n/64)] words
+    instead of uint8 [B, n].
     `p` is the decoder prior (simulate passes p/3, simulator.py:278-282).
     `out` (device path): a DecodeResult of matching device tensors to write
     into instead of allocating (steady-state loops allocate nothing).
@@ -78,30 +101,36 @@ def decode_batch(H, syndromes, p, max_iter, layers=None, algo="MS", beta=0.75, e
         code = _lib.code_for(H, dev.index)
         sched = code.schedule(layer_ptr, layer_rows)
         syn = syndromes.contiguous()
-        if syn.dtype != torch.uint8 or syn.dim() != 2 or syn.shape[1] != m:
-            raise ValueError(f"syndromes must be uint8 [B, {m}]")
+        wm, wn = (m + 63) // 64, (n + 63) // 64
+        if syn.dim() == 2 and syn.dtype == torch.uint8 and syn.shape[1] == m:
+            syn_fmt = _lib.FMT_BYTES
+        elif syn.dim() == 2 and syn.dtype == torch.int64 and syn.shape[1] == wm:
+            syn_fmt = _lib.FMT_BITS
+        else:
+            raise ValueError(f"syndromes must be uint8 [B, {m}] or int64 words [B, {wm}]")
         B = syn.shape[0]
+        e_shape, e_dtype = ((B, wn), torch.int64) if ehat_bits else ((B, n), torch.uint8)
         if out is not None:
             ehat, iters, flags, post = out.ehat, out.iters, out.flags, out.post if want_post else None
-            ok = (ehat.shape == (B, n) and ehat.dtype == torch.uint8 and iters.shape == (B,) and
+            ok = (ehat.shape == e_shape and ehat.dtype == e_dtype and iters.shape == (B,) and
                   iters.dtype == torch.int32 and flags.shape == (B,) and flags.dtype == torch.int32 and
                   all(t.device == dev and t.is_contiguous() for t in (ehat, iters, flags)) and
                   (not want_post or (post is not None and post.shape == (B, n) and
                                      post.dtype == torch.float64 and post.device == dev and
                                      post.is_contiguous())))
             if not ok:
-                raise ValueError("out buffers do not match the batch (uint8 [B, n], int32 [B], "
-                                 "int32 [B], float64 [B, n] if want_post) on the syndromes' device")
+                raise ValueError("out buffers do not match the batch (uint8 [B, n] or int64 [B, ceil(n/64)], "
+                                 "int32 [B], int32 [B], float64 [B, n] if want_post) on the syndromes' device")
         else:
-            ehat = torch.empty((B, n), dtype=torch.uint8, device=dev)
+            ehat = torch.empty(e_shape, dtype=e_dtype, device=dev)
             iters = torch.empty(B, dtype=torch.int32, device=dev)
             flags = torch.empty(B, dtype=torch.int32, device=dev)
             post = torch.empty((B, n), dtype=torch.float64, device=dev) if want_post else None
         st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
-        _lib.check(_lib.lib.qldpc_decode_device(
-            code.handle, sched.handle, _lib.ALGO[algo], syn.data_ptr(), B, float(p), int(max_iter),
-            float(beta), float(eps), ehat.data_ptr(), iters.data_ptr(),
-            post.data_ptr() if post is not None else None, flags.data_ptr(), st))
+        _lib.check(_lib.lib.qldpc_decode_device_ex(
+            code.handle, sched.handle, _lib.ALGO[algo], syn.data_ptr(), syn_fmt, B, float(p), int(max_iter),
+            float(beta), float(eps), ehat.data_ptr(), _lib.FMT_BITS if ehat_bits else _lib.FMT_BYTES,
+            iters.data_ptr(), post.data_ptr() if post is not None else None, flags.data_ptr(), st))
         return DecodeResult(ehat, iters, post, flags)
 
     syn = np.ascontiguousarray(syndromes)

@@ -136,15 +136,22 @@ class DeviceChannel:
     def _stream(self):
         return self.torch.cuda.current_stream(self.dev).cuda_stream
 
-    def sample(self, p, B):
+    def sample(self, p, B, bits=False):
+        """`bits`: syndromes as int64 words [B, ceil(m/64)] (decode_batch
+        reads either format) instead of uint8 [B, m]."""
         torch = self.torch
         errX = torch.empty((B, self.W), dtype=torch.int64, device=self.dev)
         errZ = torch.empty((B, self.W), dtype=torch.int64, device=self.dev)
-        sy_z = torch.empty((B, self.mz), dtype=torch.uint8, device=self.dev)
-        sy_x = torch.empty((B, self.mx), dtype=torch.uint8, device=self.dev)
-        _lib.check(_lib.lib.qldpc_channel_sample(
+        if bits:
+            sy_z = torch.empty((B, (self.mz + 63) // 64), dtype=torch.int64, device=self.dev)
+            sy_x = torch.empty((B, (self.mx + 63) // 64), dtype=torch.int64, device=self.dev)
+        else:
+            sy_z = torch.empty((B, self.mz), dtype=torch.uint8, device=self.dev)
+            sy_x = torch.empty((B, self.mx), dtype=torch.uint8, device=self.dev)
+        _lib.check(_lib.lib.qldpc_channel_sample_ex(
             self.cx.handle, self.cz.handle, float(p), self.seed, self.shot, int(B), errX.data_ptr(),
-            errZ.data_ptr(), sy_z.data_ptr(), sy_x.data_ptr(), self._stream()))
+            errZ.data_ptr(), sy_z.data_ptr(), sy_x.data_ptr(), _lib.FMT_BITS if bits else _lib.FMT_BYTES,
+            self._stream()))
         self.shot += int(B)
         return sy_z, sy_x, errX, errZ
 
@@ -162,14 +169,19 @@ class DeviceChannel:
             acc = torch.zeros(len(COUNTER_KEYS), dtype=torch.int64, device=self.dev)
         B = sy_z.shape[0]
         ts = (sy_z, sy_x, errX, errZ, eX, eZ, itX, itZ)
+        syn_bits = sy_z.dtype == torch.int64
+        e_bits = eX.dtype == torch.int64
+        e_shape = (B, self.W) if e_bits else (B, self.n)
         if not all(t.is_contiguous() and t.device == self.dev for t in ts) or \
-                eX.shape != (B, self.n) or eZ.shape != (B, self.n) or errX.shape != (B, self.W) or \
-                eX.dtype != torch.uint8 or itX.dtype != torch.int32 or itZ.dtype != torch.int32:
+                eX.shape != e_shape or eZ.shape != e_shape or errX.shape != (B, self.W) or \
+                eX.dtype not in (torch.uint8, torch.int64) or eZ.dtype != eX.dtype or \
+                sy_x.dtype != sy_z.dtype or itX.dtype != torch.int32 or itZ.dtype != torch.int32:
             raise ValueError("count_device: buffers do not match the batch layout")
-        _lib.check(_lib.lib.qldpc_count_outcomes(
+        F = lambda b: _lib.FMT_BITS if b else _lib.FMT_BYTES  # noqa: E731
+        _lib.check(_lib.lib.qldpc_count_outcomes_ex(
             self.cx.handle, self.cz.handle, int(B), errX.data_ptr(), errZ.data_ptr(), sy_z.data_ptr(),
-            sy_x.data_ptr(), eX.data_ptr(), eZ.data_ptr(), itX.data_ptr(), itZ.data_ptr(),
-            acc.data_ptr(), self._stream()))
+            sy_x.data_ptr(), F(syn_bits), eX.data_ptr(), eZ.data_ptr(), F(e_bits), itX.data_ptr(),
+            itZ.data_ptr(), acc.data_ptr(), self._stream()))
         return acc
 
     def count(self, sy_z, sy_x, errX, errZ, eX, eZ, itX, itZ):
@@ -183,6 +195,12 @@ def _device_ok():
         return torch.cuda.is_available()
     except ImportError:
         return False
+
+
+def _grouped_off():
+    """ms_layered_grp_kernel (opt-in, QLDPC_MS_GROUPS > 1) writes byte estimates only."""
+    import os
+    return os.environ.get("QLDPC_MS_GROUPS", "1") in ("", "1")
 
 
 def _channel_ok(Hx, Hz):
@@ -270,12 +288,15 @@ def simulate_p(Hx: np.ndarray, Hz: np.ndarray, p: float, shots: int = 1000, decT
             cur = None
             if done < my_shots:
                 B = min(batch_size, my_shots - done)
-                sy_z, sy_x, errX, errZ = ch.sample(p, B)
+                # bit-packed syndromes and estimates (one bit per check / qubit
+                # in HBM) unless OSD needs byte rows of the failing shots
+                packed = osd < 0 and _grouped_off()
+                sy_z, sy_x, errX, errZ = ch.sample(p, B, bits=packed)
                 want_post = osd >= 0
                 rX = decoders.decode_batch(Hz, sy_z, p / 3, decIterations, algo=decType, want_post=want_post,
-                                           layer_ptr=lpX, layer_rows=lrX)
+                                           layer_ptr=lpX, layer_rows=lrX, ehat_bits=packed)
                 rZ = decoders.decode_batch(Hx, sy_x, p / 3, decIterations, algo=decType, want_post=want_post,
-                                           layer_ptr=lpZ, layer_rows=lrZ)
+                                           layer_ptr=lpZ, layer_rows=lrZ, ehat_bits=packed)
                 cur = [sy_z, sy_x, errX, errZ, rX, rZ, None]
                 done += B
             if pending is not None:

@@ -3,21 +3,6 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_osd.py tests/test_gpu_simulator.py -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/ab5_pytest.log 2>&1 || { echo "pytest failed"; tail -60 gpurun_out/ab5_pytest.log; exit 1; }
-tail -2 gpurun_out/ab5_pytest.log
-cat > /tmp/sim5.py <<'PY'
-import json, os, sys, time
-sys.path.insert(0, os.getcwd())
-from qldpcsim_amd import codes, simulator
-Hx, Hz = codes.load_code("LP118_2")
-for p in (0.05, 0.1):
-    for env in ("0", "1"):
-        os.environ["QLDPC_OSD_HOST_ORDER"] = env
-        kw = dict(shots=1 << 20, decType="MS", decIterations=50, decSchedule="L", OSDorder=0, verbose=False)
-        simulator.simulate_p(Hx, Hz, p, rngSeed=2, **kw)
-        t0 = time.perf_counter()
-        r = simulator.simulate_p(Hx, Hz, p, rngSeed=1, **kw)
-        dt = time.perf_counter() - t0
-        print(json.dumps({"p": p, "host_order_only": env, "shots_per_s": (1 << 20) / dt, **r}), flush=True)
-PY
-timeout -k 10 600 python /tmp/sim5.py 2>&1 | tee gpurun_out/ab5_sim.jsonl || exit 1
+timeout -k 10 300 python tools/bench_configs.py --osd 2>&1 | tee gpurun_out/ab7_osd.jsonl || exit 1
+timeout -k 10 -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/ab7_pmc -o c -- python3 tools/bench_configs.py --osd > gpurun_out/ab7_pmc.log 2>&1 || exit 1
+timeout -k 10 -s KILL 120 rocprofv3 --pmc SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INST_LEVEL_LDS --output-format csv -d gpurun_out/ab7_pmc2 -o c -- python3 tools/bench_configs.py --osd > gpurun_out/ab7_pmc2.log 2>&1 || exit 1
