@@ -1,0 +1,50 @@
+"""The decoder as a registered PyTorch operator (qldpcsim_amd/ops.py):
+registration, shape inference on meta tensors, loud failure on CPU tensors
+(no CPU path); on the GPU, equality with decode_batch."""
+import numpy as np
+import pytest
+import torch
+
+from qldpcsim_amd import codes, ops, schedule  # noqa: F401  (registers torch.ops.qldpc)
+
+
+def _args(code="LP118_0", sched="L"):
+    Hx, Hz = codes.load_code(code)
+    lx, _ = schedule.select_layers(Hx, Hz, sched)
+    lp, lr = schedule.pack_layers(lx, Hz.shape[0])
+    return Hz, torch.as_tensor(Hz), torch.as_tensor(lp), torch.as_tensor(lr)
+
+
+def test_op_is_registered_and_infers_shapes_on_meta():
+    Hz, H, lp, lr = _args()
+    m, n = Hz.shape
+    syn = torch.empty((17, m), dtype=torch.uint8, device="meta")
+    e, it, post, fl = torch.ops.qldpc.decode(syn, H, lp, lr, 0.01, 10, "MS", 0.75, 1e-9, True, False)
+    assert e.shape == (17, n) and e.dtype == torch.uint8 and it.shape == (17,) and it.dtype == torch.int32
+    assert post.shape == (17, n) and post.dtype == torch.float64 and fl.shape == (17,)
+    words = torch.empty((5, (m + 63) // 64), dtype=torch.int64, device="meta")
+    e, it, post, fl = torch.ops.qldpc.decode(words, H, lp, lr, 0.01, 10, "BP", 0.75, 1e-9, False, True)
+    assert e.shape == (5, (n + 63) // 64) and e.dtype == torch.int64 and post.shape == (5, 0)
+
+
+def test_op_refuses_cpu_tensors():
+    Hz, H, lp, lr = _args()
+    with pytest.raises(ValueError, match="HIP device"):
+        torch.ops.qldpc.decode(torch.zeros((2, Hz.shape[0]), dtype=torch.uint8), H, lp, lr, 0.01, 5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("code,sched,algo", [("LP118_0", "F", "MS"), ("LP118_2", "L", "MS"), ("LP04_0", "L", "BP")])
+def test_op_equals_decode_batch(code, sched, algo):
+    from qldpcsim_amd import decoders
+    Hz, H, lp, lr = _args(code, sched)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    syn = torch.randint(0, 2, (2048, Hz.shape[0]), dtype=torch.uint8, device="cuda", generator=g)
+    e, it, post, fl = torch.ops.qldpc.decode(syn, H, lp, lr, 0.02, 20, algo, 0.75, 1e-9, True, False)
+    ref = decoders.decode_batch(Hz, syn, 0.02, 20, algo=algo, layer_ptr=lp.numpy(), layer_rows=lr.numpy(),
+                                want_post=True)
+    assert torch.equal(e, ref.ehat) and torch.equal(it, ref.iters) and torch.equal(fl, ref.flags)
+    assert torch.equal(post, ref.post)
+    eb, itb, _, _ = torch.ops.qldpc.decode(decoders.pack_bits(syn), H, lp, lr, 0.02, 20, algo, 0.75, 1e-9,
+                                          False, True)
+    assert torch.equal(decoders.unpack_bits(eb, Hz.shape[1]), ref.ehat) and torch.equal(itb, ref.iters)

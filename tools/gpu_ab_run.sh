@@ -3,6 +3,8 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python tools/bench_configs.py --osd 2>&1 | tee gpurun_out/ab7_osd.jsonl || exit 1
-timeout -k 10 -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/ab7_pmc -o c -- python3 tools/bench_configs.py --osd > gpurun_out/ab7_pmc.log 2>&1 || exit 1
-timeout -k 10 -s KILL 120 rocprofv3 --pmc SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INST_LEVEL_LDS --output-format csv -d gpurun_out/ab7_pmc2 -o c -- python3 tools/bench_configs.py --osd > gpurun_out/ab7_pmc2.log 2>&1 || exit 1
+timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/ab8_pytest.log 2>&1 || { echo "pytest failed"; tail -60 gpurun_out/ab8_pytest.log; exit 1; }
+tail -2 gpurun_out/ab8_pytest.log
+for io in bytes bits; do timeout -k 10 300 python bench.py --steps 10 --warmup 3 --cpu-seconds 0 --io $io > gpurun_out/ab8_bench_$io.log 2>&1 || exit 1; python -c "import json;d=json.loads(open('gpurun_out/ab8_bench_$io.log').read().strip().splitlines()[-1]);print('$io',d['value'],d['roofline']['kernel_ms_per_launch'])"; done
+timeout -k 10 -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/ab8_w -o c -- python3 bench.py --steps 1 --warmup 0 --cpu-seconds 0 > gpurun_out/ab8_w.log 2>&1 || exit 1
+timeout -k 10 -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/ab8_f -o c -- python3 bench.py --steps 1 --warmup 0 --cpu-seconds 0 > gpurun_out/ab8_f.log 2>&1 || exit 1
