@@ -69,6 +69,7 @@ struct qldpc_code {
   int uniform_deg = 0;  // row degree if every row has it, else 0
   int max_row_deg = 0, max_col_deg = 0;
   int rank = 0;         // GF(2) rank of H (gf2math.rank), for OSD
+  bool zero_col = false;  // H has an all-zero column (GPU OSD: exact REF kernel only)
   std::vector<int32_t> row_ptr, col_idx;     // CSR, np.where(H) order
   std::vector<int32_t> vperm, vinv;          // relabeled -> original, original -> relabeled
   std::vector<int32_t> csc_ptr, csc_edge;    // relabeled-variable CSC: CSR edge ids, ascending check
@@ -156,6 +157,7 @@ extern "C" int qldpc_code_create(const uint8_t* h_H, int m, int n, qldpc_code** 
     for (int e = c->row_ptr[r]; e < c->row_ptr[r + 1]; ++e)
       c->col_bits[(size_t)c->col_idx[e] * c->mw + (r >> 6)] |= 1ull << (r & 63);
   c->rank = gf2_rank_cols(c->col_bits, n, c->mw);
+  for (int j = 0; j < n && !c->zero_col; ++j) c->zero_col = cdeg[j] == 0;
   c->wc.resize(m);
   for (int r = 0; r < m; ++r) {
     uint64_t z = 0x9E3779B97F4A7C15ull * (uint64_t)(r + 1) + 0xD1B54A32D192ED03ull;   // splitmix64
@@ -1168,13 +1170,13 @@ static int setdiff_table_ints(int n) {
 }
 
 static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t* d_syn, const int32_t* d_perm,
-                           const int32_t* d_tiepos, int order, uint8_t* d_ehat, int32_t* d_status,
-                           void* stream);
+                           const int32_t* d_tiepos, const double* d_post, int order, uint8_t* d_ehat,
+                           int32_t* d_status, void* stream);
 
 extern "C" int qldpc_osd_device(const qldpc_code* code, int64_t count, const uint8_t* d_syn,
                                 const int32_t* d_perm, int order, uint8_t* d_ehat, int32_t* d_status,
                                 void* stream) {
-  return osd_device_impl(code, count, d_syn, d_perm, nullptr, order, d_ehat, d_status, stream);
+  return osd_device_impl(code, count, d_syn, d_perm, nullptr, nullptr, order, d_ehat, d_status, stream);
 }
 
 extern "C" int qldpc_osd_order_device(const qldpc_code* code, int64_t count, const double* d_post,
@@ -1202,12 +1204,12 @@ extern "C" int qldpc_osd_device_ordered(const qldpc_code* code, int64_t count, c
                                         int32_t* d_perm, int32_t* d_tiepos, void* stream) {
   int rc = qldpc_osd_order_device(code, count, d_post, d_perm, d_tiepos, stream);
   if (rc != QLDPC_OK) return rc;
-  return osd_device_impl(code, count, d_syn, d_perm, d_tiepos, order, d_ehat, d_status, stream);
+  return osd_device_impl(code, count, d_syn, d_perm, d_tiepos, d_post, order, d_ehat, d_status, stream);
 }
 
 static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t* d_syn, const int32_t* d_perm,
-                           const int32_t* d_tiepos, int order, uint8_t* d_ehat, int32_t* d_status,
-                           void* stream) {
+                           const int32_t* d_tiepos, const double* d_post, int order, uint8_t* d_ehat,
+                           int32_t* d_status, void* stream) {
   if (!code) return fail(QLDPC_EINVAL, "code is null");
   if (count < 0) return fail(QLDPC_EINVAL, "negative count");
   if (count == 0) return QLDPC_OK;
@@ -1216,16 +1218,29 @@ static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t*
   const int m = code->m, n = code->n;
   if (m > 1024) return fail(QLDPC_EUNSUP, "GPU OSD supports m <= 1024 rows (got %d)", m);
   const int nw = qldpc::osd_nw_of((n + 1 + 63) / 64);
-  const void* k = qldpc::select_osd_kernel(nw);
-  if (!k) return fail(QLDPC_EUNSUP, "GPU OSD supports n <= 2111 columns (got %d)", n);
-  int lds = 4 * n + 4 * (m + 2) + n;
-  lds = align16(lds) + 8 * nw * (1 + 2 * 16 + 2) + 4 * 32 + 16;  // emask, candidate / xrow rows, slots
-  if (order == 1) lds += 4 * setdiff_table_ints(n);
+  const void* kcol = qldpc::select_osd_kernel(nw);
+  if (!kcol) return fail(QLDPC_EUNSUP, "GPU OSD supports n <= 2111 columns (got %d)", n);
+  // The block kernel picks pivot rows by row index instead of REF's row
+  // order: same J, same e_J (the unique solution), except when column 0 of
+  // H[:, perm] has no pivot (an all-zero column of H: column kernel for the
+  // whole code) or the syndrome lies outside H's column space (the block
+  // kernel marks those shots, a second column-kernel pass redoes them).
+  // QLDPC_OSD_KERNEL=column: the column kernel alone (A/B reference).
+  const char* kenv = getenv("QLDPC_OSD_KERNEL");
+  const bool column = (kenv && strcmp(kenv, "column") == 0) || code->zero_col;
+  const void* kblk = column ? nullptr : qldpc::select_osd_block_kernel(nw, m);
+  const int block = std::max(64, (m + 63) / 64 * 64);
+  const int base = align16(4 * n + 4 * (m + 2) + n) + (order == 1 ? 4 * setdiff_table_ints(n) : 0);
+  const int lds_col = base + 8 * nw * (1 + 2 * 16 + 2) + 4 * 32 + 16;         // emask, candidate / xrow rows, slots, misc
+  const int lds_blk = base + 8 * nw * (1 + 64) + 8 * 64 + 8 * 2 * block + 4 * 3 * block + 4 * 64 + 32;
+                      // emask, PW, CT, Wd / Cm, pkof / pidx / crow, pk, misc
   int dev = 0, max_lds = 0;
   HIP_TRY(hipGetDevice(&dev));
   HIP_TRY(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
-  if (lds > max_lds) return fail(QLDPC_EUNSUP, "GPU OSD needs %d B LDS", lds);
-  HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds));
+  if (lds_col > max_lds) return fail(QLDPC_EUNSUP, "GPU OSD needs %d B LDS", lds_col);
+  HIP_TRY(hipFuncSetAttribute(kcol, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds));
+  if (kblk && lds_blk > max_lds) kblk = nullptr;
+  if (kblk) HIP_TRY(hipFuncSetAttribute(kblk, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds));
   qldpc::OsdArgs a{};
   a.row_ptr = code->d_row_ptr;
   a.col_idx = code->d_col_idx;
@@ -1238,7 +1253,13 @@ static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t*
   a.rank = code->rank;
   a.order = order;
   a.tiepos = d_tiepos;
-  const int block = std::max(64, (m + 63) / 64 * 64);
+  a.post = d_tiepos ? d_post : nullptr;
+  static unsigned long long* d_prof = nullptr;       // diagnostic builds (QLDPC_OSD_TIMING)
+  if (getenv("QLDPC_OSD_PROF") && !d_prof) {
+    HIP_TRY(hipMalloc(&d_prof, 16 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(d_prof, 0, 16 * sizeof(unsigned long long)));
+  }
+  a.prof = d_prof;
   int64_t done = 0;
   while (done < count) {  // grid.x limit
     const int64_t g = std::min<int64_t>(count - done, 1 << 30);
@@ -1248,9 +1269,23 @@ static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t*
     ai.ehat = d_ehat + done * n;
     ai.status = d_status + done;
     if (ai.tiepos) ai.tiepos = d_tiepos + done;
+    if (ai.post) ai.post = d_post + done * n;
     void* params[] = {(void*)&ai};
-    HIP_TRY(hipLaunchKernel(k, dim3((unsigned)g), dim3(block), params, (size_t)lds, (hipStream_t)stream));
+    if (kblk) {
+      HIP_TRY(hipLaunchKernel(kblk, dim3((unsigned)g), dim3(block), params, (size_t)lds_blk, (hipStream_t)stream));
+      ai.redo = 1;                                    // same stream: runs after the block pass
+    }
+    HIP_TRY(hipLaunchKernel(kcol, dim3((unsigned)g), dim3(block), params, (size_t)lds_col, (hipStream_t)stream));
     done += g;
+  }
+  if (d_prof) {
+    unsigned long long h[16];
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    HIP_TRY(hipMemcpy(h, d_prof, sizeof(h), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemset(d_prof, 0, sizeof(h)));
+    fprintf(stderr, "osd_prof shots=%lld", (long long)count);
+    for (int i = 0; i < 14; ++i) fprintf(stderr, " %.0f", (double)h[i] / (double)count);
+    fprintf(stderr, "\n");
   }
   return QLDPC_OK;
 }

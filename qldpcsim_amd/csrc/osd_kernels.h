@@ -12,10 +12,16 @@ struct OsdArgs {
   const uint8_t* syn;      // [count][m]
   uint8_t* ehat;           // [count][n] in/out
   int32_t* status;         // [count] 0 ok, 1 = reference IndexError case, 2 = order not certified
+                           // (3 = internal: osd_block_kernel hands the shot to osd_kernel)
   const int32_t* tiepos;   // [count] or null: first sorted position t whose key gap to t+1 is
                            // within the certification margin (osd_order_kernel); with it, a
                            // shot whose decision prefix reaches tiepos is left untouched (status 2)
+  const double* post;      // [count][n] posteriors behind tiepos' order (osd_block_kernel's
+                           // tie-run certification), with tiepos
   int m, n, rank, order;
+  unsigned long long* prof; // QLDPC_OSD_TIMING builds only: per-phase cycle sums
+  int redo;                // osd_kernel only: process just the shots whose status is 3
+                           // (left by osd_block_kernel: syndrome outside H's column space)
 };
 
 // Reliability order on the device (decoders.py:320-325): keys
@@ -33,6 +39,7 @@ constexpr int kOrderMarginUlp = 64;
 hipError_t launch_osd_order(const OrderArgs& a, long long count, hipStream_t stream);
 
 const void* select_osd_kernel(int nw);  // nw = 64-bit words per row incl. the syndrome column
+const void* select_osd_block_kernel(int nw, int m);  // block elimination (default), same arguments
 int osd_nw_of(int nw);
 
 }  // namespace qldpc

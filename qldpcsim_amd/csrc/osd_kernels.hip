@@ -30,6 +30,28 @@ namespace qldpc {
 
 __device__ int first_setdiff(int n, const unsigned char* inJ, int nJ, int* table);
 
+// Sort key of one posterior as NumPy forms it in decoders.py:320-325 (clip,
+// exp, 1 / (1 + e), max(prob, 1 - prob)), with the device exp: the key lies
+// in [0.5, 1], so bits(key) - bits(0.5) (< 2^53) orders like the key itself.
+// kBadKey for a NaN posterior.
+constexpr uint64_t kBadKey = ~0ull;
+__device__ __forceinline__ uint64_t order_key(double x) {
+  x = x < -100.0 ? -100.0 : (x > 100.0 ? 100.0 : x);   // np.clip(P, -100, 100)
+  const double e = exp(x);
+  const double prob = 1.0 / (1.0 + e);
+  const double q = 1.0 - prob;
+  const double rel = prob > q ? prob : q;             // np.maximum(prob, 1 - prob)
+  if (!(rel >= 0.5 && rel <= 1.0)) return kBadKey;
+  return __builtin_bit_cast(uint64_t, rel) - 0x3FE0000000000000ull;   // bits of 0.5
+}
+
+#ifndef QLDPC_OSD_TIMING
+#define QLDPC_OSD_TIMING 0  // diagnostic builds: osd_block_kernel sums per-phase cycles into a.prof
+#endif
+#ifndef QLDPC_ABLATE_OSD
+#define QLDPC_ABLATE_OSD 0  // timing-only builds of osd_block_kernel: bit 0 skips phase D, bit 1 the engine
+#endif
+
 template <int NW>
 __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
   // LDS: inv_perm[n] | J list [m+2] | inJ bytes [n] | emask [NW] u64 |
@@ -52,6 +74,7 @@ __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
   const int t = threadIdx.x;
   const int lane = t & 63, wave = t >> 6, nwaves = blockDim.x >> 6;
   const long long shot = blockIdx.x;
+  if (a.redo && a.status[shot] != 3) return;       // second pass after osd_block_kernel
   const int32_t* perm = a.perm + shot * (long long)n;
   const uint8_t* syn = a.syn + shot * (long long)m;
   uint8_t* ehat = a.ehat + shot * (long long)n;
@@ -213,6 +236,403 @@ __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Block elimination (the default GPU OSD): one workgroup barrier per 64-column
+// word instead of one per column (osd_kernel spends most of its instructions
+// on that per-column protocol). Thread t owns row t of Hp (+ syndrome).
+//
+// Pivot rows are chosen by row index (the first unused row holding a 1), not
+// by REF's row order. That changes T but not what OSD reads from it: the
+// pivot columns J are the columns independent of their predecessors (a
+// property of Hp), and the fully reduced pivot row of column j_k gives the
+// k-th entry of e_J = the unique solution of H_J x = s + H_I e_I (DESIGN.md
+// §3, OSD). Two cases need REF's own order and go to osd_kernel instead: an
+// all-zero column 0 (the host never selects this kernel for an H with a zero
+// column) and a syndrome outside the column space of H (status 3 here, then
+// osd_kernel redoes those shots in the same stream).
+//
+// Per word w:
+//   A  every row publishes its word w
+//   B  wave 0 runs the elimination over the 64 columns of word w alone on
+//      that copy (row 64 s + lane in slot s): word value, and C = the set of
+//      this block's pivot rows (by block-start value) XOR-ed into it so far.
+//      Column i: pivot = first unused row with a 1 (ballots), every other row
+//      with a 1 is XOR-ed with it: word ^= pivot word, C ^= C_pivot ^ {pivot}.
+//      Columns no unused row holds are skipped unseen: XORs among unused rows
+//      never set a bit that none of them held.
+//   C  the block's pivot rows publish their words w.. (still block-start values)
+//   D  every row applies its C to words w..: each update added a current
+//      pivot row = its block-start value + earlier pivot rows of the block.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_or32(uint32_t x) {
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xf, 0xf, false);  // row_half_mirror
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xf, 0xf, false);  // row_mirror
+  return (uint32_t)(__builtin_amdgcn_readlane((int)x, 0) | __builtin_amdgcn_readlane((int)x, 16) |
+                    __builtin_amdgcn_readlane((int)x, 32) | __builtin_amdgcn_readlane((int)x, 48));
+}
+
+// Phase B over the columns `cols` of one half-word (HI: bits 32..63, read
+// from hi[]) on the first SF compact slots, straight-line per column: one
+// ballot per slot (SGPR lane masks) masked by the still-free rows, the first
+// hit by scalar selects, the pivot's values by uniform slot select +
+// readlane, the elimination under exec masks. Pivot k's compact position and
+// column bit go to pk[k]; returns the pivot count K.
+template <int SL, int SF, bool HI>
+__device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL], uint32_t (&cl)[SL],
+                                          uint32_t (&ch)[SL], uint32_t& frv, uint32_t cols, int K,
+                                          int w, int lane, int& rank, int& nJ, bool& done, uint64_t& pivm,
+                                          int rankH, int m, int* pk, int* Jl, unsigned char* inJ) {
+  while (cols && !done) {
+    const int bit = (int)__builtin_ctz(cols);
+    cols &= cols - 1;
+    const uint32_t bm = 1u << bit;
+    int f = 0x7fffffff;
+#pragma unroll
+    for (int s = SF - 1; s >= 0; --s) {
+      const uint64_t c = __ballot(((HI ? hi[s] : lo[s]) & bm) != 0 && ((frv >> s) & 1u));
+      f = c ? 64 * s + (int)__builtin_ctzll(c) : f;
+    }
+    f = __builtin_amdgcn_readfirstlane(f);
+    if (f == 0x7fffffff) continue;                 // dependent column: not in J
+    const int fs = f >> 6, fl = f & 63;
+    const uint32_t plo = __builtin_amdgcn_readlane((int)lo[fs], fl);
+    const uint32_t phi = __builtin_amdgcn_readlane((int)hi[fs], fl);
+    uint32_t pcl = __builtin_amdgcn_readlane((int)cl[fs], fl);
+    uint32_t pch = __builtin_amdgcn_readlane((int)ch[fs], fl);
+    if (K < 32) pcl ^= 1u << K;
+    else pch ^= 1u << (K - 32);
+    const bool notme = lane != fl;
+    if (!notme) frv &= ~(1u << fs);
+#pragma unroll
+    for (int s = 0; s < SF; ++s) {
+      if (((HI ? hi[s] : lo[s]) & bm) != 0 && (s != fs || notme)) {   // rows holding a 1,
+        lo[s] ^= plo;                                                  // above and below
+        hi[s] ^= phi;
+        cl[s] ^= pcl;
+        ch[s] ^= pch;
+      }
+    }
+    const int wb = (HI ? 32 : 0) + bit;
+    const int i = 64 * w + wb;
+    pivm |= 1ull << wb;
+    if (lane == 0) {
+      pk[K] = (f << 6) | wb;
+      if (i != 0) {
+        Jl[nJ] = i;
+        inJ[i] = 1;
+      }
+    }
+    if (i != 0) ++nJ;
+    ++K;
+    ++rank;
+    if (rank >= rankH || rank >= m) done = true;
+    if (i == 0 && done) rank = -1;                  // column 0 alone reaches rank(H): the
+  }                                                 // greedy loop never breaks (:333-342)
+  return K;
+}
+
+// block_half on the smallest power-of-two slot count >= SF (code per count)
+template <int SL, int SFMAX, bool HI>
+__device__ __forceinline__ int block_half_n(int SF, uint32_t (&lo)[SL], uint32_t (&hi)[SL], uint32_t (&cl)[SL],
+                                            uint32_t (&ch)[SL], uint32_t& frv, uint32_t cols, int K,
+                                            int w, int lane, int& rank, int& nJ, bool& done, uint64_t& pivm,
+                                            int rankH, int m, int* pk, int* Jl, unsigned char* inJ) {
+  if constexpr (SFMAX > 1) {
+    if (SF <= SFMAX / 2)
+      return block_half_n<SL, SFMAX / 2, HI>(SF, lo, hi, cl, ch, frv, cols, K, w, lane, rank, nJ, done, pivm,
+                                             rankH, m, pk, Jl, inJ);
+  }
+  return block_half<SL, SFMAX, HI>(lo, hi, cl, ch, frv, cols, K, w, lane, rank, nJ, done, pivm, rankH, m, pk,
+                                   Jl, inJ);
+}
+
+// SL = rows per wave-0 lane (m <= 64 SL), sized to the code so the state stays
+// in VGPRs
+template <int NW, int SL>
+__global__ void __launch_bounds__(1024) osd_block_kernel(OsdArgs a) {
+  // LDS: inv_perm[n] | J list [m+2] | inJ bytes [n] | emask [NW] | Wd [MR] | Cm [MR] |
+  //      PW [64][NW] | CT [64] | pkof [MR] | pidx [MR] | crow [MR] | pk [64] | misc [8] | set table
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int m = a.m, n = a.n;
+  const int MR = blockDim.x;
+  int* inv = (int*)lds;
+  int* Jl = inv + n;
+  unsigned char* inJ = (unsigned char*)(Jl + m + 2);
+  uint64_t* emask = (uint64_t*)(lds + ((4 * (n + m + 2) + n + 15) & ~15));
+  uint64_t* Wd = emask + NW;
+  uint64_t* Cm = Wd + MR;
+  uint64_t* PW = Cm + MR;                            // [64][NW]
+  uint64_t* CT = PW + 64 * NW;                       // C of this block's pivot by its column bit
+  int* pkof = (int*)(CT + 64);                       // pivot tag per row: 64 w + k, -1 none
+  int* pidx = pkof + MR;                             // pivot index of each row (m: none)
+  int* crow = pidx + MR;                             // compact position -> row (free rows)
+  int* pk = crow + MR;                               // pivot k: compact position << 6 | column bit
+  int* misc = pk + 64;                               // [0] nJ [1] rank [2] i0 [3] flag [4] done [5] K
+  int* table = misc + 8;                             // [6..7] this block's pivot-column mask
+
+  const int t = threadIdx.x;
+  // readfirstlane: `wave` is then known to be wave-uniform, so the engine's
+  // branch is scalar and the counters it updates stay in SGPRs
+  const int lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const bool own = t < m;
+  const long long shot = blockIdx.x;
+  const int32_t* perm = a.perm + shot * (long long)n;
+  const uint8_t* syn = a.syn + shot * (long long)m;
+  uint8_t* ehat = a.ehat + shot * (long long)n;
+
+  for (int i = t; i < n; i += blockDim.x) {
+    inv[perm[i]] = i;
+    inJ[i] = 0;
+  }
+  pkof[t] = -1;
+  pidx[t] = m;
+  if (t == 0) misc[3] = 0;
+  __syncthreads();
+
+  // my row of Hp (+ syndrome bit at column n)
+  uint64_t R[NW];
+#pragma unroll
+  for (int w = 0; w < NW; ++w) R[w] = 0;
+  if (own) {
+    for (int e = a.row_ptr[t]; e < a.row_ptr[t + 1]; ++e) {
+      const int i = inv[a.col_idx[e]];
+#pragma unroll
+      for (int w = 0; w < NW; ++w)
+        if ((i >> 6) == w) R[w] |= 1ull << (i & 63);
+    }
+    if (syn[t] & 1) {
+#pragma unroll
+      for (int w = 0; w < NW; ++w)
+        if ((n >> 6) == w) R[w] |= 1ull << (n & 63);
+    }
+  }
+
+  int rank = 0, nJ = 1;
+  bool done = a.rank == 0;                            // rank(H) = 0: IndexError below
+  if (t == 0) {
+    Jl[0] = 0;                                        // column 0 always (decoders.py:329)
+    inJ[0] = 1;
+  }
+
+  // runtime block loop (one copy of phase B); R is only ever indexed by the
+  // compile-time x of the unrolled word loops, so it stays in VGPRs
+  unsigned long long tp[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long tc = QLDPC_OSD_TIMING ? clock64() : 0;
+#define QLDPC_TICK(k)                            \
+  if constexpr (QLDPC_OSD_TIMING != 0) {         \
+    const unsigned long long now = clock64();    \
+    tp[k] += now - tc;                           \
+    tc = now;                                    \
+  }
+  QLDPC_TICK(0);                                      // setup
+  for (int w = 0; w < NW && 64 * w < n && !done; ++w) {   // done: uniform, re-read per block
+    if (own) {                                        // A
+      uint64_t v = 0;
+#pragma unroll
+      for (int x = 0; x < NW; ++x)
+        if (x == w) v = R[x];
+      Wd[t] = v;
+    }
+    __syncthreads();
+    QLDPC_TICK(1);
+    if (wave == 0) {                                  // B
+      // the engine works on the rows still free (no pivot yet), compacted:
+      // crow[c] = the c-th free row; earlier pivots are reduced in phase D
+      const int rank0 = rank;
+      int F = 0;
+#pragma unroll
+      for (int s = 0; s < SL; ++s) {
+        const int row = 64 * s + lane;
+        const bool fr = row < m && pidx[row] == m;
+        const uint64_t bf = __ballot(fr);
+        if (fr) crow[F + __builtin_amdgcn_mbcnt_hi((uint32_t)(bf >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bf, 0))] = row;
+        F += __builtin_popcountll(bf);
+      }
+      uint32_t lo[SL], hi[SL], cl[SL], ch[SL];
+      uint32_t frv = 0;                               // bit s: compact row 64 s + lane not yet a pivot
+      uint32_t alo = 0, ahi = 0;                      // columns some free row holds
+#pragma unroll
+      for (int s = 0; s < SL; ++s) {
+        const int cp = 64 * s + lane;
+        const uint64_t v = cp < F ? Wd[crow[cp]] : 0ull;
+        lo[s] = (uint32_t)v;
+        hi[s] = (uint32_t)(v >> 32);
+        cl[s] = ch[s] = 0;
+        frv |= cp < F ? 1u << s : 0u;
+        alo |= lo[s];
+        ahi |= hi[s];
+      }
+      uint64_t cols = ((uint64_t)wave_or32(ahi) << 32) | wave_or32(alo);
+      if (n - 64 * w < 64) cols &= (1ull << (n - 64 * w)) - 1;
+      if constexpr ((QLDPC_ABLATE_OSD & 2) != 0) cols = 0;
+      const int SF = (F + 63) >> 6;
+      uint64_t pivm = 0;
+      // low half-word columns, then high (each loop's column order ascends)
+      int K = block_half_n<SL, SL, false>(SF, lo, hi, cl, ch, frv, (uint32_t)cols, 0, w, lane, rank, nJ, done,
+                                          pivm, a.rank, m, pk, Jl, inJ);
+      K = block_half_n<SL, SL, true>(SF, lo, hi, cl, ch, frv, (uint32_t)(cols >> 32), K, w, lane, rank, nJ, done,
+                                     pivm, a.rank, m, pk, Jl, inJ);
+#pragma unroll
+      for (int s = 0; s < SL; ++s) {
+        const int cp = 64 * s + lane;
+        if (cp < F) Cm[crow[cp]] = ((uint64_t)ch[s] << 32) | cl[s];
+      }
+      // (one wave: its LDS accesses complete in order, so these reads see
+      // the writes above)
+      if (lane < K) {
+        const int e = pk[lane];
+        const int row = crow[e >> 6];
+        CT[e & 63] = Cm[row] ^ (1ull << lane);        // reduced pivot k = its own row + C
+        pkof[row] = 64 * w + lane;
+        pidx[row] = rank0 + lane;                     // REF moves the k-th pivot row to row k
+      }
+      if (lane == 0) {
+        misc[0] = nJ;
+        misc[1] = rank;
+        misc[4] = done;
+        misc[5] = K;
+        misc[6] = (int)(uint32_t)pivm;
+        misc[7] = (int)(uint32_t)(pivm >> 32);
+      }
+    }
+    QLDPC_TICK(2);
+    __syncthreads();
+    QLDPC_TICK(3);
+    nJ = __builtin_amdgcn_readfirstlane(misc[0]);    // (LDS loads count as per-lane values)
+    rank = __builtin_amdgcn_readfirstlane(misc[1]);
+    done = __builtin_amdgcn_readfirstlane(misc[4]) != 0;
+    const int K = __builtin_amdgcn_readfirstlane(misc[5]);
+    const uint64_t pivm = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(misc[7]) << 32) |
+                          (uint32_t)__builtin_amdgcn_readfirstlane(misc[6]);
+    // C: pivot rows publish their words w.. as they were at the block start
+    const int tag = own ? pkof[t] : -1;
+    if (tag >= 0 && (tag >> 6) == w) {
+      uint64_t* dst = PW + (tag & 63) * NW;
+#pragma unroll
+      for (int x = 0; x < NW; ++x)
+        if (x >= w) dst[x] = R[x];
+    }
+    __syncthreads();
+    QLDPC_TICK(4);
+    // D: every row applies its combination of this block's pivot rows
+    if (own && K > 0 && (QLDPC_ABLATE_OSD & 1) == 0) {
+      uint64_t cm;
+      if (tag >= 0 && (tag >> 6) < w) {
+        // a pivot row of an earlier block: clear this block's pivot columns
+        // from it. Its result is unique (word w + the reduced block pivots it
+        // holds a 1 for), so C = XOR of those pivots' C (no engine pass).
+        uint64_t v = 0;
+#pragma unroll
+        for (int x = 0; x < NW; ++x)
+          if (x == w) v = R[x];
+        v &= pivm;
+        cm = 0;
+        while (v) {
+          cm ^= CT[__builtin_ctzll(v)];
+          v &= v - 1;
+        }
+      } else {
+        cm = Cm[t];
+      }
+      while (cm) {
+        const int k = (int)__builtin_ctzll(cm);
+        cm &= cm - 1;
+        const uint64_t* src = PW + k * NW;
+#pragma unroll
+        for (int x = 0; x < NW; ++x)
+          if (x >= w) R[x] ^= src[x];
+      }
+    }
+    QLDPC_TICK(5);
+  }
+  if constexpr (QLDPC_OSD_TIMING != 0) {
+    if (lane == 0 && wave < 2)
+      for (int k = 0; k < 6; ++k) atomicAdd(a.prof + 8 * wave + k, tp[k]);
+  }
+#undef QLDPC_TICK
+  if (rank < a.rank) {                              // greedy loop runs past column n-1
+    if (t == 0) a.status[shot] = 1;                 // (the reference raises IndexError)
+    return;
+  }
+  // a row left without pivot is zero on every column of H; a 1 in its
+  // syndrome column means s is outside H's column space (status 3)
+  const int mypos = own ? pidx[t] : m;
+  uint64_t sbit = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w)
+    if (w == (n >> 6)) sbit = (R[w] >> (n & 63)) & 1ull;   // (compile-time R index)
+  if (own && mypos >= nJ && sbit) misc[3] = 1;
+  if (t == 0) {
+    int i0 = -1;
+    if (a.order == 1 && nJ < n) i0 = first_setdiff(n, inJ, nJ, table);   // (decoders.py:344)
+    misc[2] = i0;
+    misc[5] = 0;
+    misc[6] = a.tiepos && a.tiepos[shot] <= max(Jl[nJ - 1], i0);
+  }
+  __syncthreads();
+  const int i0 = misc[2];
+  if (misc[6]) {
+    // The device order may differ from NumPy's only inside runs of near-equal
+    // keys (adjacent gaps within the margin; NumPy's exp / tie order can
+    // permute a run). The result stands if every such run that meets the
+    // decision prefix lies inside the eliminated columns [0, J_last], holds
+    // neither position 0 (always in J) nor the order-1 flip position, and is
+    // all-pivot or all-non-pivot: then every order of the run gives the same
+    // set J (an all-pivot run is independent modulo the columns before it, an
+    // all-non-pivot run lies in their span) and the same e (the solution of
+    // the same system). Anything else: status 2, NumPy's order on the host.
+    const int jlast = Jl[nJ - 1];
+    uint64_t* key = PW;                               // n keys (PW is free: 512 NW >= 8 n bytes)
+    bool fail = false;
+    for (int i = t; i < n; i += blockDim.x) {
+      const uint64_t k = order_key(a.post[shot * (long long)n + perm[i]]);
+      fail |= k == kBadKey;
+      key[i] = k;
+    }
+    __syncthreads();
+    for (int i = t; i + 1 < n; i += blockDim.x) {
+      if (key[i + 1] - key[i] > (uint64_t)kOrderMarginUlp) continue;   // not a near-tie pair
+      const bool flip = i == i0 || i + 1 == i0;
+      if (i > jlast) fail |= flip;                    // both outside J: only the flip position
+      else fail |= i == 0 || i + 1 > jlast || inJ[i] != inJ[i + 1] || flip;
+    }
+    if (fail) misc[5] = 1;
+    __syncthreads();
+    if (misc[5]) {
+      if (t == 0) a.status[shot] = 2;
+      return;
+    }
+  }
+  if (misc[3]) {
+    if (t == 0) a.status[shot] = 3;
+    return;
+  }
+  // information-set values e_I (e_perm = e_hat[perm], decoders.py:345)
+  for (int i0w = 64 * wave; i0w < 64 * NW; i0w += blockDim.x) {
+    const int i = i0w + lane;
+    const bool bit = i < n && !inJ[i] && (ehat[perm[i]] & 1);
+    const uint64_t bits = __ballot(bit);
+    if (lane == 0) emask[i0w >> 6] = bits;
+  }
+  __syncthreads();
+  if (t == 0 && i0 >= 0) emask[i0 >> 6] ^= 1ull << (i0 & 63);   // order-1 flip (:349-350)
+  __syncthreads();
+  // e_J = (T sJ)[:|J|]: the k-th pivot row gives entry k   (decoders.py:352-358)
+  if (own && mypos < nJ) {
+    uint64_t acc = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      if (w == (n >> 6)) acc ^= (R[w] >> (n & 63)) & 1ull;      // T s (augmented column)
+      acc ^= (uint64_t)(__builtin_popcountll(R[w] & emask[w]) & 1);
+    }
+    ehat[perm[Jl[mypos]]] = (uint8_t)(acc & 1ull);            // e_hat[perm] = ... (:368)
+  }
+  if (t == 0 && i0 >= 0) ehat[perm[i0]] ^= 1;
+  if (t == 0) a.status[shot] = 0;
+}
+
+// ---------------------------------------------------------------------------
 // Reliability order of one shot per workgroup (np2 / 2 threads): keys as
 // NumPy forms them in decoders.py:320-325 (clip, exp, 1 / (1 + e),
 // max(prob, 1 - prob)), with the device exp; a key lies in [0.5, 1], so
@@ -230,20 +650,13 @@ __global__ void __launch_bounds__(1024) osd_order_kernel(OrderArgs a) {
   const long long shot = blockIdx.x;
   const double* post = a.post + shot * (long long)a.n;
   const int n = a.n, np2 = a.np2;
-  constexpr uint64_t kHalf = 0x3FE0000000000000ull;  // bits of 0.5
   bool bad = false;
   for (int i = t; i < np2; i += nt) {
     uint64_t c = ~0ull;                               // padding sorts last
     if (i < n) {
-      double x = post[i];
-      x = x < -100.0 ? -100.0 : (x > 100.0 ? 100.0 : x);   // np.clip(P, -100, 100)
-      const double e = exp(x);
-      const double prob = 1.0 / (1.0 + e);
-      const double q = 1.0 - prob;
-      const double rel = prob > q ? prob : q;         // np.maximum(prob, 1 - prob)
-      if (!(rel >= 0.5 && rel <= 1.0)) bad = true;    // NaN posterior: host decides
-      const uint64_t u = (__builtin_bit_cast(uint64_t, rel) - kHalf) & ((1ull << 53) - 1);
-      c = (u << 11) | (uint64_t)i;
+      const uint64_t u = order_key(post[i]);
+      if (u == kBadKey) bad = true;                   // NaN posterior: host decides
+      c = ((u & ((1ull << 53) - 1)) << 11) | (uint64_t)i;
     }
     key[i] = c;
   }
@@ -360,6 +773,22 @@ const void* select_osd_kernel(int nw) {
   if (nw <= 9) return (const void*)&osd_kernel<9>;
   if (nw <= 17) return (const void*)&osd_kernel<17>;
   if (nw <= 33) return (const void*)&osd_kernel<33>;
+  return nullptr;
+}
+
+template <int NW>
+static const void* osd_block_by_rows(int m) {
+  if (m <= 256) return (const void*)&osd_block_kernel<NW, 4>;
+  if (m <= 512) return (const void*)&osd_block_kernel<NW, 8>;
+  return nullptr;                                   // (the engine state would spill: column kernel)
+}
+
+// block kernel configurations whose state fits the VGPR budget without
+// spills (m <= 512 rows, n <= 1087 columns); null -> osd_kernel
+const void* select_osd_block_kernel(int nw, int m) {
+  if (nw <= 4) return osd_block_by_rows<4>(m);
+  if (nw <= 9) return osd_block_by_rows<9>(m);
+  if (nw <= 17) return osd_block_by_rows<17>(m);
   return nullptr;
 }
 

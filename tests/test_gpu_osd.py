@@ -161,3 +161,94 @@ def test_ordered_device_osd_equals_numpy_ordered_osd(code, p, order):
                                 torch.zeros(k, dtype=torch.int32, device="cuda"))
     decoders.apply_osd_device(H, s_d, res, order)
     np.testing.assert_array_equal(res.ehat.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("code", ["LP04_0", "LP118_2", "bicycle"])
+def test_block_kernel_matches_column_kernel(code, monkeypatch):
+    """The block elimination (pivots by row index, default) and the exact-REF
+    column kernel (QLDPC_OSD_KERNEL=column) agree shot for shot, on consistent
+    and inconsistent syndromes (the latter take the column kernel's second
+    pass inside the block path)."""
+    from qldpcsim_amd import codes
+    Hx, _ = codes.load_code(code)
+    rng = np.random.default_rng(5)
+    k = 96
+    syn = rng.integers(0, 2, (k, Hx.shape[0])).astype(np.uint8)
+    err = (rng.random((k // 2, Hx.shape[1])) < 0.06).astype(np.int64)
+    syn[: k // 2] = (err @ Hx.T.astype(np.int64)) % 2
+    post = rng.normal(0, 3, (k, Hx.shape[1]))
+    e0 = (post < 0).astype(np.uint8)
+    for order in (0, 1):
+        blk, sb = _gpu_osd(Hx, syn, e0, post, order)
+        monkeypatch.setenv("QLDPC_OSD_KERNEL", "column")
+        col, sc = _gpu_osd(Hx, syn, e0, post, order)
+        monkeypatch.delenv("QLDPC_OSD_KERNEL")
+        assert np.all(sb == 0) and np.all(sc == 0)
+        np.testing.assert_array_equal(blk, col)
+
+
+def test_osd_zero_column_code():
+    """An H with an all-zero column: the reference reads e_J off REF's own row
+    order when column 0 of H[:, perm] has no pivot, so such codes use the
+    column kernel; results equal the host OSD."""
+    from qldpcsim_amd import _lib, codes, decoders
+    Hx, _ = codes.load_code("steane")
+    H = np.concatenate([np.zeros((Hx.shape[0], 1), Hx.dtype), Hx], axis=1)
+    # a redundant row: rank(H) < m, so e_J's extra entry (J holds the zero
+    # column besides rank(H) pivots) reads a non-pivot row, as REF leaves them
+    # (with rank(H) = m the reference's e_J assignment itself fails to broadcast)
+    H = np.concatenate([H, (H[:1] + H[1:2]) % 2], axis=0)
+    rng = np.random.default_rng(11)
+    k = 32
+    syn = rng.integers(0, 2, (k, H.shape[0])).astype(np.uint8)
+    post = rng.normal(0, 3, (k, H.shape[1]))
+    post[: k // 2, 0] = 0.0                                  # the zero column first in the order
+    e0 = (post < 0).astype(np.uint8)
+    for order in (0, 1):
+        got, st = _gpu_osd(H, syn, e0, post, order)
+        want = e0.copy()
+        perms = np.ascontiguousarray(decoders.osd_perms(post), np.int32)
+        code_h = _lib.code_for(H)
+        _lib.check(_lib.lib.qldpc_osd_decode_batch(code_h.handle, k, _lib.ptr(syn), _lib.ptr(perms),
+                                                   order, _lib.ptr(want), 1))
+        assert np.all(st == 0)
+        np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("code,order", [("LP118_2", 0), ("LP118_0", 1), ("LP04_0", 0)])
+def test_ordered_device_osd_tie_runs(code, order):
+    """Posteriors with many exact and near ties: every shot the device path
+    certifies (status 0) equals the host OSD under NumPy's order, including
+    shots whose decision prefix holds tie runs (certified by the run test:
+    all-pivot / all-non-pivot runs inside the eliminated prefix)."""
+    import torch
+    from qldpcsim_amd import _lib, decoders
+    H, syn, e, post = _decoded_posteriors(code, 0.1 if code != "LP04_0" else 0.12, 800, 30, 13)
+    rng = np.random.default_rng(4)
+    q = post.copy()
+    for r in range(0, len(q), 2):                              # exact tie pairs among the least
+        idx = np.argsort(np.abs(q[r]), kind="stable")[4:24]    # reliable columns (inside the
+        q[r, idx[1::2]] = q[r, idx[0::2]]                      # decision prefix)
+    q[2::8] = np.round(q[2::8] * 2) / 2                         # tie-heavy rows
+    q[1::4] += rng.normal(0, 1e-14, q[1::4].shape)             # near ties (within the margin)
+    k = len(q)
+    code_h = _lib.code_for(H, 0)
+    d = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a, dt), device="cuda")  # noqa: E731
+    s_d, p_d, e_d = d(syn, np.uint8), d(q, np.float64), d(e, np.uint8)
+    st = torch.empty(k, dtype=torch.int32, device="cuda")
+    perm = torch.empty((k, H.shape[1]), dtype=torch.int32, device="cuda")
+    tie = torch.empty(k, dtype=torch.int32, device="cuda")
+    _lib.check(_lib.lib.qldpc_osd_device_ordered(code_h.handle, k, s_d.data_ptr(), p_d.data_ptr(), order,
+                                                 e_d.data_ptr(), st.data_ptr(), perm.data_ptr(), tie.data_ptr(),
+                                                 None))
+    got, status, tie = e_d.cpu().numpy(), st.cpu().numpy(), tie.cpu().numpy()
+    want = e.copy()
+    perms = np.ascontiguousarray(decoders.osd_perms(q), np.int32)
+    _lib.check(_lib.lib.qldpc_osd_decode_batch(_lib.code_for(H).handle, k, _lib.ptr(syn), _lib.ptr(perms),
+                                               order, _lib.ptr(want), 1))
+    assert set(np.unique(status)) <= {0, 2}
+    ok = status == 0
+    np.testing.assert_array_equal(got[ok], want[ok])
+    np.testing.assert_array_equal(got[~ok], e[~ok])
+    # the run test certifies shots whose order has ties well inside the prefix
+    assert (ok & (tie < H.shape[1] // 2)).sum() > 0

@@ -3,8 +3,6 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/ab8_pytest.log 2>&1 || { echo "pytest failed"; tail -60 gpurun_out/ab8_pytest.log; exit 1; }
-tail -2 gpurun_out/ab8_pytest.log
-for io in bytes bits; do timeout -k 10 300 python bench.py --steps 10 --warmup 3 --cpu-seconds 0 --io $io > gpurun_out/ab8_bench_$io.log 2>&1 || exit 1; python -c "import json;d=json.loads(open('gpurun_out/ab8_bench_$io.log').read().strip().splitlines()[-1]);print('$io',d['value'],d['roofline']['kernel_ms_per_launch'])"; done
-timeout -k 10 -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/ab8_w -o c -- python3 bench.py --steps 1 --warmup 0 --cpu-seconds 0 > gpurun_out/ab8_w.log 2>&1 || exit 1
-timeout -k 10 -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/ab8_f -o c -- python3 bench.py --steps 1 --warmup 0 --cpu-seconds 0 > gpurun_out/ab8_f.log 2>&1 || exit 1
+T=ab17
+QLDPC_OSD_PROF=1 QLDPC_LIB=$PWD/qldpcsim_amd/_build/var_prof.so timeout -k 10 300 python tools/osd_bench.py LP118_2 MS L 50 0.1 131072 0 2 > gpurun_out/${T}.log 2>&1 || { tail -20 gpurun_out/${T}.log; exit 1; }
+grep osd_prof gpurun_out/${T}.log | tail -3; tail -1 gpurun_out/${T}.log
