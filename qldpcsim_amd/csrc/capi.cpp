@@ -1228,11 +1228,14 @@ static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t*
   // QLDPC_OSD_KERNEL=column: the column kernel alone (A/B reference).
   const char* kenv = getenv("QLDPC_OSD_KERNEL");
   const bool column = (kenv && strcmp(kenv, "column") == 0) || code->zero_col;
-  const void* kblk = column ? nullptr : qldpc::select_osd_block_kernel(nw, m);
+  int rt = 1;                                        // block kernel: rows per thread
+  const void* kblk = column ? nullptr : qldpc::select_osd_block_kernel(nw, m, &rt);
   const int block = std::max(64, (m + 63) / 64 * 64);
+  const int bblk = std::max(64, ((m + rt - 1) / rt + 63) / 64 * 64);   // block kernel threads
+  const int mr = rt * bblk;                          // its row slots
   const int base = align16(4 * n + 4 * (m + 2) + n) + (order == 1 ? 4 * setdiff_table_ints(n) : 0);
   const int lds_col = base + 8 * nw * (1 + 2 * 16 + 2) + 4 * 32 + 16;         // emask, candidate / xrow rows, slots, misc
-  const int lds_blk = base + 8 * nw * (1 + 64) + 8 * 64 + 8 * 2 * block + 4 * 3 * block + 4 * 64 + 32;
+  const int lds_blk = base + 8 * nw * (1 + 64) + 8 * 64 + 8 * 2 * mr + 4 * 3 * mr + 4 * 64 + 32;
                       // emask, PW, CT, Wd / Cm, pkof / pidx / crow, pk, misc
   int dev = 0, max_lds = 0;
   HIP_TRY(hipGetDevice(&dev));
@@ -1272,7 +1275,7 @@ static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t*
     if (ai.post) ai.post = d_post + done * n;
     void* params[] = {(void*)&ai};
     if (kblk) {
-      HIP_TRY(hipLaunchKernel(kblk, dim3((unsigned)g), dim3(block), params, (size_t)lds_blk, (hipStream_t)stream));
+      HIP_TRY(hipLaunchKernel(kblk, dim3((unsigned)g), dim3(bblk), params, (size_t)lds_blk, (hipStream_t)stream));
       ai.redo = 1;                                    // same stream: runs after the block pass
     }
     HIP_TRY(hipLaunchKernel(kcol, dim3((unsigned)g), dim3(block), params, (size_t)lds_col, (hipStream_t)stream));

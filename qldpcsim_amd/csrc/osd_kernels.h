@@ -39,7 +39,7 @@ constexpr int kOrderMarginUlp = 64;
 hipError_t launch_osd_order(const OrderArgs& a, long long count, hipStream_t stream);
 
 const void* select_osd_kernel(int nw);  // nw = 64-bit words per row incl. the syndrome column
-const void* select_osd_block_kernel(int nw, int m);  // block elimination (default), same arguments
+const void* select_osd_block_kernel(int nw, int m, int* rows_per_thread);  // block elimination (default), same arguments
 int osd_nw_of(int nw);
 
 }  // namespace qldpc

@@ -284,17 +284,31 @@ __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL]
                                           int w, int lane, int& rank, int& nJ, bool& done, uint64_t& pivm,
                                           int rankH, int m, int* pk, int* Jl, unsigned char* inJ) {
   while (cols && !done) {
-    const int bit = (int)__builtin_ctz(cols);
-    cols &= cols - 1;
-    const uint32_t bm = 1u << bit;
-    int f = 0x7fffffff;
+    // loop-carried scalars re-asserted wave-uniform: otherwise the compiler
+    // keeps them per lane and turns the loop into an exec-masked one
+    cols = (uint32_t)__builtin_amdgcn_readfirstlane((int)cols);
+    K = __builtin_amdgcn_readfirstlane(K);
+    rank = __builtin_amdgcn_readfirstlane(rank);
+    nJ = __builtin_amdgcn_readfirstlane(nJ);
+    pivm = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pivm >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pivm);
+    // next column with a pivot: the search loop only reads the state, so
+    // skipping dependent columns costs no register copies at the joins
+    int f = 0x7fffffff, bit = 0;
+    while (cols) {
+      bit = (int)__builtin_ctz(cols);
+      cols &= cols - 1;
+      const uint32_t bm = 1u << bit;
 #pragma unroll
-    for (int s = SF - 1; s >= 0; --s) {
-      const uint64_t c = __ballot(((HI ? hi[s] : lo[s]) & bm) != 0 && ((frv >> s) & 1u));
-      f = c ? 64 * s + (int)__builtin_ctzll(c) : f;
+      for (int s = SF - 1; s >= 0; --s) {
+        const uint64_t c = __ballot(((HI ? hi[s] : lo[s]) & bm) != 0 && ((frv >> s) & 1u));
+        f = c ? 64 * s + (int)__builtin_ctzll(c) : f;
+      }
+      f = __builtin_amdgcn_readfirstlane(f);
+      if (f != 0x7fffffff) break;                   // (dependent columns: not in J)
     }
-    f = __builtin_amdgcn_readfirstlane(f);
-    if (f == 0x7fffffff) continue;                 // dependent column: not in J
+    if (f == 0x7fffffff) break;
+    const uint32_t bm = 1u << bit;
     const int fs = f >> 6, fl = f & 63;
     const uint32_t plo = __builtin_amdgcn_readlane((int)lo[fs], fl);
     const uint32_t phi = __builtin_amdgcn_readlane((int)hi[fs], fl);
@@ -328,7 +342,8 @@ __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL]
     ++rank;
     if (rank >= rankH || rank >= m) done = true;
     if (i == 0 && done) rank = -1;                  // column 0 alone reaches rank(H): the
-  }                                                 // greedy loop never breaks (:333-342)
+    done = __builtin_amdgcn_readfirstlane((int)done) != 0;   // greedy loop never breaks (:333-342)
+  }
   return K;
 }
 
@@ -348,14 +363,16 @@ __device__ __forceinline__ int block_half_n(int SF, uint32_t (&lo)[SL], uint32_t
 }
 
 // SL = rows per wave-0 lane (m <= 64 SL), sized to the code so the state stays
-// in VGPRs
-template <int NW, int SL>
-__global__ void __launch_bounds__(1024) osd_block_kernel(OsdArgs a) {
+// in VGPRs; RT = rows per thread (thread t holds rows t, t + blockDim, ..):
+// with 2, a 450-row shot takes 4 waves and a CU holds 4 shots (4 engines, one
+// per SIMD) instead of 2
+template <int NW, int SL, int RT>
+__global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_eu(RT == 2 ? 3 : 1))) osd_block_kernel(OsdArgs a) {
   // LDS: inv_perm[n] | J list [m+2] | inJ bytes [n] | emask [NW] | Wd [MR] | Cm [MR] |
   //      PW [64][NW] | CT [64] | pkof [MR] | pidx [MR] | crow [MR] | pk [64] | misc [8] | set table
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int m = a.m, n = a.n;
-  const int MR = blockDim.x;
+  const int B = blockDim.x, MR = RT * B;
   int* inv = (int*)lds;
   int* Jl = inv + n;
   unsigned char* inJ = (unsigned char*)(Jl + m + 2);
@@ -375,7 +392,6 @@ __global__ void __launch_bounds__(1024) osd_block_kernel(OsdArgs a) {
   // readfirstlane: `wave` is then known to be wave-uniform, so the engine's
   // branch is scalar and the counters it updates stay in SGPRs
   const int lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const bool own = t < m;
   const long long shot = blockIdx.x;
   const int32_t* perm = a.perm + shot * (long long)n;
   const uint8_t* syn = a.syn + shot * (long long)m;
@@ -385,26 +401,35 @@ __global__ void __launch_bounds__(1024) osd_block_kernel(OsdArgs a) {
     inv[perm[i]] = i;
     inJ[i] = 0;
   }
-  pkof[t] = -1;
-  pidx[t] = m;
+#pragma unroll
+  for (int h = 0; h < RT; ++h) {
+    pkof[t + h * B] = -1;
+    pidx[t + h * B] = m;
+  }
   if (t == 0) misc[3] = 0;
   __syncthreads();
 
-  // my row of Hp (+ syndrome bit at column n)
-  uint64_t R[NW];
+  // my rows of Hp (+ syndrome bit at column n)
+  uint64_t R[RT][NW];
+  bool own[RT];
 #pragma unroll
-  for (int w = 0; w < NW; ++w) R[w] = 0;
-  if (own) {
-    for (int e = a.row_ptr[t]; e < a.row_ptr[t + 1]; ++e) {
-      const int i = inv[a.col_idx[e]];
+  for (int h = 0; h < RT; ++h) {
+    const int r = t + h * B;
+    own[h] = r < m;
 #pragma unroll
-      for (int w = 0; w < NW; ++w)
-        if ((i >> 6) == w) R[w] |= 1ull << (i & 63);
-    }
-    if (syn[t] & 1) {
+    for (int w = 0; w < NW; ++w) R[h][w] = 0;
+    if (own[h]) {
+      for (int e = a.row_ptr[r]; e < a.row_ptr[r + 1]; ++e) {
+        const int i = inv[a.col_idx[e]];
 #pragma unroll
-      for (int w = 0; w < NW; ++w)
-        if ((n >> 6) == w) R[w] |= 1ull << (n & 63);
+        for (int w = 0; w < NW; ++w)
+          if ((i >> 6) == w) R[h][w] |= 1ull << (i & 63);
+      }
+      if (syn[r] & 1) {
+#pragma unroll
+        for (int w = 0; w < NW; ++w)
+          if ((n >> 6) == w) R[h][w] |= 1ull << (n & 63);
+      }
     }
   }
 
@@ -427,13 +452,15 @@ __global__ void __launch_bounds__(1024) osd_block_kernel(OsdArgs a) {
   }
   QLDPC_TICK(0);                                      // setup
   for (int w = 0; w < NW && 64 * w < n && !done; ++w) {   // done: uniform, re-read per block
-    if (own) {                                        // A
-      uint64_t v = 0;
 #pragma unroll
-      for (int x = 0; x < NW; ++x)
-        if (x == w) v = R[x];
-      Wd[t] = v;
-    }
+    for (int h = 0; h < RT; ++h)                      // A
+      if (own[h]) {
+        uint64_t v = 0;
+#pragma unroll
+        for (int x = 0; x < NW; ++x)
+          if (x == w) v = R[h][x];
+        Wd[t + h * B] = v;
+      }
     __syncthreads();
     QLDPC_TICK(1);
     if (wave == 0) {                                  // B
@@ -506,26 +533,32 @@ __global__ void __launch_bounds__(1024) osd_block_kernel(OsdArgs a) {
     const uint64_t pivm = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(misc[7]) << 32) |
                           (uint32_t)__builtin_amdgcn_readfirstlane(misc[6]);
     // C: pivot rows publish their words w.. as they were at the block start
-    const int tag = own ? pkof[t] : -1;
-    if (tag >= 0 && (tag >> 6) == w) {
-      uint64_t* dst = PW + (tag & 63) * NW;
+    int tag[RT];
 #pragma unroll
-      for (int x = 0; x < NW; ++x)
-        if (x >= w) dst[x] = R[x];
+    for (int h = 0; h < RT; ++h) {
+      tag[h] = own[h] ? pkof[t + h * B] : -1;
+      if (tag[h] >= 0 && (tag[h] >> 6) == w) {
+        uint64_t* dst = PW + (tag[h] & 63) * NW;
+#pragma unroll
+        for (int x = 0; x < NW; ++x)
+          if (x >= w) dst[x] = R[h][x];
+      }
     }
     __syncthreads();
     QLDPC_TICK(4);
     // D: every row applies its combination of this block's pivot rows
-    if (own && K > 0 && (QLDPC_ABLATE_OSD & 1) == 0) {
+#pragma unroll
+    for (int h = 0; h < RT; ++h)
+    if (own[h] && K > 0 && (QLDPC_ABLATE_OSD & 1) == 0) {
       uint64_t cm;
-      if (tag >= 0 && (tag >> 6) < w) {
+      if (tag[h] >= 0 && (tag[h] >> 6) < w) {
         // a pivot row of an earlier block: clear this block's pivot columns
         // from it. Its result is unique (word w + the reduced block pivots it
         // holds a 1 for), so C = XOR of those pivots' C (no engine pass).
         uint64_t v = 0;
 #pragma unroll
         for (int x = 0; x < NW; ++x)
-          if (x == w) v = R[x];
+          if (x == w) v = R[h][x];
         v &= pivm;
         cm = 0;
         while (v) {
@@ -533,15 +566,17 @@ __global__ void __launch_bounds__(1024) osd_block_kernel(OsdArgs a) {
           v &= v - 1;
         }
       } else {
-        cm = Cm[t];
+        cm = Cm[t + h * B];
       }
+      // (per-lane gathers of the pivot rows: a uniform loop over all K with
+      // broadcast reads measured 2x slower, VALU-bound)
       while (cm) {
         const int k = (int)__builtin_ctzll(cm);
         cm &= cm - 1;
         const uint64_t* src = PW + k * NW;
 #pragma unroll
         for (int x = 0; x < NW; ++x)
-          if (x >= w) R[x] ^= src[x];
+          if (x >= w) R[h][x] ^= src[x];
       }
     }
     QLDPC_TICK(5);
@@ -557,12 +592,16 @@ __global__ void __launch_bounds__(1024) osd_block_kernel(OsdArgs a) {
   }
   // a row left without pivot is zero on every column of H; a 1 in its
   // syndrome column means s is outside H's column space (status 3)
-  const int mypos = own ? pidx[t] : m;
-  uint64_t sbit = 0;
+  int mypos[RT];
 #pragma unroll
-  for (int w = 0; w < NW; ++w)
-    if (w == (n >> 6)) sbit = (R[w] >> (n & 63)) & 1ull;   // (compile-time R index)
-  if (own && mypos >= nJ && sbit) misc[3] = 1;
+  for (int h = 0; h < RT; ++h) {
+    mypos[h] = own[h] ? pidx[t + h * B] : m;
+    uint64_t sbit = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w)
+      if (w == (n >> 6)) sbit = (R[h][w] >> (n & 63)) & 1ull;   // (compile-time R index)
+    if (own[h] && mypos[h] >= nJ && sbit) misc[3] = 1;
+  }
   if (t == 0) {
     int i0 = -1;
     if (a.order == 1 && nJ < n) i0 = first_setdiff(n, inJ, nJ, table);   // (decoders.py:344)
@@ -619,15 +658,17 @@ __global__ void __launch_bounds__(1024) osd_block_kernel(OsdArgs a) {
   if (t == 0 && i0 >= 0) emask[i0 >> 6] ^= 1ull << (i0 & 63);   // order-1 flip (:349-350)
   __syncthreads();
   // e_J = (T sJ)[:|J|]: the k-th pivot row gives entry k   (decoders.py:352-358)
-  if (own && mypos < nJ) {
-    uint64_t acc = 0;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      if (w == (n >> 6)) acc ^= (R[w] >> (n & 63)) & 1ull;      // T s (augmented column)
-      acc ^= (uint64_t)(__builtin_popcountll(R[w] & emask[w]) & 1);
+  for (int h = 0; h < RT; ++h)
+    if (own[h] && mypos[h] < nJ) {
+      uint64_t acc = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        if (w == (n >> 6)) acc ^= (R[h][w] >> (n & 63)) & 1ull;   // T s (augmented column)
+        acc ^= (uint64_t)(__builtin_popcountll(R[h][w] & emask[w]) & 1);
+      }
+      ehat[perm[Jl[mypos[h]]]] = (uint8_t)(acc & 1ull);         // e_hat[perm] = ... (:368)
     }
-    ehat[perm[Jl[mypos]]] = (uint8_t)(acc & 1ull);            // e_hat[perm] = ... (:368)
-  }
   if (t == 0 && i0 >= 0) ehat[perm[i0]] ^= 1;
   if (t == 0) a.status[shot] = 0;
 }
@@ -777,18 +818,19 @@ const void* select_osd_kernel(int nw) {
 }
 
 template <int NW>
-static const void* osd_block_by_rows(int m) {
-  if (m <= 256) return (const void*)&osd_block_kernel<NW, 4>;
-  if (m <= 512) return (const void*)&osd_block_kernel<NW, 8>;
+static const void* osd_block_by_rows(int m, int* rt) {
+  *rt = m <= 256 ? 1 : 2;
+  if (m <= 256) return (const void*)&osd_block_kernel<NW, 4, 1>;
+  if (m <= 512) return (const void*)&osd_block_kernel<NW, 8, 2>;
   return nullptr;                                   // (the engine state would spill: column kernel)
 }
 
 // block kernel configurations whose state fits the VGPR budget without
 // spills (m <= 512 rows, n <= 1087 columns); null -> osd_kernel
-const void* select_osd_block_kernel(int nw, int m) {
-  if (nw <= 4) return osd_block_by_rows<4>(m);
-  if (nw <= 9) return osd_block_by_rows<9>(m);
-  if (nw <= 17) return osd_block_by_rows<17>(m);
+const void* select_osd_block_kernel(int nw, int m, int* rows_per_thread) {
+  if (nw <= 4) return osd_block_by_rows<4>(m, rows_per_thread);
+  if (nw <= 9) return osd_block_by_rows<9>(m, rows_per_thread);
+  if (nw <= 17) return osd_block_by_rows<17>(m, rows_per_thread);
   return nullptr;
 }
 
