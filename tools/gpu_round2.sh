@@ -19,3 +19,6 @@ bash tools/gpu_profile_roofline.sh $TAG \
   bpl2 "--code LP118_2 --algo BP --schedule L --iters 100 --p 0.05 --batch 131072" || exit 1
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_$TAG.log 2>&1 || { echo "bench failed"; exit 1; }
 tail -1 gpurun_out/bench_$TAG.log
+# device OSD (configs[3] at p = 0.1): kernel stats of the block elimination
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/osd_$TAG -o t -- python3 tools/osd_bench.py LP118_2 MS L 50 0.1 131072 0 3 > gpurun_out/osd_$TAG.log 2>&1 || { echo "osd profile failed"; exit 1; }
+tail -1 gpurun_out/osd_$TAG.log
