@@ -196,9 +196,20 @@ def osd_perms(post, nthreads=None):
     nthreads = nthreads or min(16, os.cpu_count() or 1)
     if post.shape[0] < 256 or nthreads <= 1:
         return one(post)
+    # a persistent pool (starting 16 threads per call had cost ~4 ms, more than
+    # the sorts of a few hundred rows) and chunks of >= 64 rows
+    chunks = max(1, min(4 * nthreads, post.shape[0] // 64))
+    return np.concatenate(list(_thread_pool(nthreads).map(one, np.array_split(post, chunks))))
+
+
+_POOL = {}
+
+
+def _thread_pool(n):
     from concurrent.futures import ThreadPoolExecutor
-    with ThreadPoolExecutor(nthreads) as ex:
-        return np.concatenate(list(ex.map(one, np.array_split(post, 4 * nthreads))))
+    if n not in _POOL:
+        _POOL[n] = ThreadPoolExecutor(n)
+    return _POOL[n]
 
 
 _PINNED = {}
@@ -243,6 +254,17 @@ def _host_order_only():
     return os.environ.get("QLDPC_OSD_HOST_ORDER", "") == "1"
 
 
+def _device_order_min():
+    """Fewest non-converged shots of one decode for which the reliability order
+    is computed on the device. Below it NumPy orders them on the host in one
+    pass: few shots cost the host little, the device order would add a round
+    trip (status back, then the host pass anyway for the tie-holding shots),
+    and at low p most OSD shots carry saturated posteriors, whose exact key
+    ties send them to the host regardless (LP118_2 MS-L p = 0.05: 735 of 738)."""
+    import os
+    return int(os.environ.get("QLDPC_OSD_DEVICE_MIN", "4096"))
+
+
 def osd_device_stage(items, stream=None, slot0=0, order=0):
     """First half of the device OSD: find each decode's non-converged shots
     (one device sync), then queue asynchronously on the device: the
@@ -272,7 +294,7 @@ def osd_device_stage(items, stream=None, slot0=0, order=0):
         cs = torch.cuda.current_stream(dev)
         st = stream if stream is not None else cs.cuda_stream
         status_h = _pinned(("status", slot0 + slot), (k,), torch.int32)
-        if n <= 2048 and not _host_order_only():
+        if n <= 2048 and k >= _device_order_min() and not _host_order_only():
             perm = torch.empty((k, n), dtype=torch.int32, device=dev)
             tie = torch.empty(k, dtype=torch.int32, device=dev)
             _lib.check(_lib.lib.qldpc_osd_device_ordered(code.handle, k, syn_b.data_ptr(), post_b.data_ptr(),

@@ -131,7 +131,7 @@ def test_device_order_equals_numpy_below_tiepos(code, p):
 
 
 @pytest.mark.parametrize("code,p,order", [("LP118_2", 0.1, 0), ("LP118_0", 0.08, 1), ("LP04_0", 0.12, 4)])
-def test_ordered_device_osd_equals_numpy_ordered_osd(code, p, order):
+def test_ordered_device_osd_equals_numpy_ordered_osd(code, p, order, monkeypatch):
     """qldpc_osd_device_ordered gives the NumPy-ordered result on every shot it
     decides (status 0) and leaves the rest untouched (status 2); the
     apply_osd_device path (device order + host fallback) equals the host OSD
@@ -156,7 +156,8 @@ def test_ordered_device_osd_equals_numpy_ordered_osd(code, p, order):
     np.testing.assert_array_equal(got[ok], want[ok])
     np.testing.assert_array_equal(got[~ok], e[~ok])
     assert ok.mean() > 0.5, ok.mean()
-    # the full device path with the host fallback
+    # the full device path with the host fallback (device order at any count)
+    monkeypatch.setenv("QLDPC_OSD_DEVICE_MIN", "1")
     res = decoders.DecodeResult(d(e, np.uint8), torch.zeros(k, dtype=torch.int32, device="cuda"), p_d,
                                 torch.zeros(k, dtype=torch.int32, device="cuda"))
     decoders.apply_osd_device(H, s_d, res, order)

@@ -1,7 +1,7 @@
 """End-to-end simulate_p throughput (device sampler + decode + OSD + counters)
 for BASELINE.json configs[3] / configs[4] shapes on one GPU.
 
-usage: python tools/bench_sim.py [shots]
+usage: python tools/bench_sim.py [shots] [CODE:DEC]
 """
 import json
 import os
@@ -19,7 +19,10 @@ def main():
         ("LP118_2", "BP", "L", 4, 100),     # configs[4]: BP layered (+OSD 4: ignored by simulate)
         ("LP118_0", "MS", "F", -1, 50),
     ]
+    only = sys.argv[2] if len(sys.argv) > 2 else None            # e.g. "LP118_2:MS"
     for code, dec, sched, osd, it in runs:
+        if only and only != f"{code}:{dec}":
+            continue
         Hx, Hz = codes.load_code(code)
         for p in (0.01, 0.02, 0.05, 0.1):
             simulator.simulate_p(Hx, Hz, p, shots=shots, decType=dec, decIterations=it,
