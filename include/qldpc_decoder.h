@@ -179,6 +179,18 @@ int qldpc_osd_device_ordered(const qldpc_code *code, int64_t count, const uint8_
                              int order, uint8_t *d_ehat, int32_t *d_status, int32_t *d_perm, int32_t *d_tiepos,
                              void *stream);
 
+/* qldpc_osd_device_ordered plus a spill of the shots it leaves to the host:
+ * each status-2 shot also copies its posterior row to d_spill_post[slot]
+ * (double[spill_cap][n]) and its index (0 .. count-1) to d_spill_idx[slot],
+ * slot = the next value of *d_spill_count (int32, zeroed by the caller), for
+ * slot < spill_cap; *d_spill_count ends as the number of status-2 shots. The
+ * host then fetches exactly those posteriors with one copy (no gather
+ * kernel queued behind other work). */
+int qldpc_osd_device_ordered_ex(const qldpc_code *code, int64_t count, const uint8_t *d_syn, const double *d_post,
+                                int order, uint8_t *d_ehat, int32_t *d_status, int32_t *d_perm, int32_t *d_tiepos,
+                                double *d_spill_post, int32_t *d_spill_idx, int32_t *d_spill_count,
+                                int64_t spill_cap, void *stream);
+
 /* First element of CPython's `set(range(n)) - set(J)` iteration order
  * (the reference's infoSet[0], decoders.py:344); -1 if empty. */
 int qldpc_cpython_setdiff_first(int n, const int32_t *J, int nJ);

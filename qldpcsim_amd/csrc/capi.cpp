@@ -1172,6 +1172,13 @@ static int setdiff_table_ints(int n) {
 static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t* d_syn, const int32_t* d_perm,
                            const int32_t* d_tiepos, const double* d_post, int order, uint8_t* d_ehat,
                            int32_t* d_status, void* stream);
+struct SpillCfg {
+  double* post = nullptr;
+  int32_t* idx = nullptr;
+  int32_t* count = nullptr;
+  int64_t cap = 0;
+};
+static thread_local SpillCfg g_spill;               // set by qldpc_osd_device_ordered_ex for one call
 
 extern "C" int qldpc_osd_device(const qldpc_code* code, int64_t count, const uint8_t* d_syn,
                                 const int32_t* d_perm, int order, uint8_t* d_ehat, int32_t* d_status,
@@ -1202,9 +1209,24 @@ extern "C" int qldpc_osd_order_device(const qldpc_code* code, int64_t count, con
 extern "C" int qldpc_osd_device_ordered(const qldpc_code* code, int64_t count, const uint8_t* d_syn,
                                         const double* d_post, int order, uint8_t* d_ehat, int32_t* d_status,
                                         int32_t* d_perm, int32_t* d_tiepos, void* stream) {
+  return qldpc_osd_device_ordered_ex(code, count, d_syn, d_post, order, d_ehat, d_status, d_perm, d_tiepos,
+                                     nullptr, nullptr, nullptr, 0, stream);
+}
+
+extern "C" int qldpc_osd_device_ordered_ex(const qldpc_code* code, int64_t count, const uint8_t* d_syn,
+                                           const double* d_post, int order, uint8_t* d_ehat, int32_t* d_status,
+                                           int32_t* d_perm, int32_t* d_tiepos, double* d_spill_post,
+                                           int32_t* d_spill_idx, int32_t* d_spill_count, int64_t spill_cap,
+                                           void* stream) {
+  if (d_spill_count && (!d_spill_post || !d_spill_idx || spill_cap < 0))
+    return fail(QLDPC_EINVAL, "spill buffers incomplete");
+  if (d_spill_count && count > INT32_MAX) return fail(QLDPC_EINVAL, "spill indices are int32");
   int rc = qldpc_osd_order_device(code, count, d_post, d_perm, d_tiepos, stream);
   if (rc != QLDPC_OK) return rc;
-  return osd_device_impl(code, count, d_syn, d_perm, d_tiepos, d_post, order, d_ehat, d_status, stream);
+  g_spill = {d_spill_post, d_spill_idx, d_spill_count, spill_cap};
+  rc = osd_device_impl(code, count, d_syn, d_perm, d_tiepos, d_post, order, d_ehat, d_status, stream);
+  g_spill = {};
+  return rc;
 }
 
 static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t* d_syn, const int32_t* d_perm,
@@ -1257,6 +1279,12 @@ static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t*
   a.order = order;
   a.tiepos = d_tiepos;
   a.post = d_tiepos ? d_post : nullptr;
+  if (d_tiepos && g_spill.count) {
+    a.spill_post = g_spill.post;
+    a.spill_idx = g_spill.idx;
+    a.spill_count = g_spill.count;
+    a.spill_cap = g_spill.cap;
+  }
   static unsigned long long* d_prof = nullptr;       // diagnostic builds (QLDPC_OSD_TIMING)
   if (getenv("QLDPC_OSD_PROF") && !d_prof) {
     HIP_TRY(hipMalloc(&d_prof, 16 * sizeof(unsigned long long)));
@@ -1273,6 +1301,7 @@ static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t*
     ai.status = d_status + done;
     if (ai.tiepos) ai.tiepos = d_tiepos + done;
     if (ai.post) ai.post = d_post + done * n;
+    ai.shot_base = done;
     void* params[] = {(void*)&ai};
     if (kblk) {
       HIP_TRY(hipLaunchKernel(kblk, dim3((unsigned)g), dim3(bblk), params, (size_t)lds_blk, (hipStream_t)stream));

@@ -1726,14 +1726,14 @@ __device__ __forceinline__ uint32_t cn_bp_group(const DecodeArgs& a, const LdsVi
   double th = 1.0;
   if (ek) th = qldpc_tanh((pj - c2v[p]) / 2.0);           // v2c (:269), tanh (:254)
   // np.prod: sequential left fold over the check's edges in ascending variable
-  // order; lane s multiplies the running product of lanes 0..s-1 by its t_s
-  double acc = th;
+  // order, ((t_0 t_1) t_2) ..., formed redundantly by every lane of the group
+  // from the group's t values (one permute each): same rounding as a
+  // lane-to-lane prefix chain, without its per-step index arithmetic, selects
+  // and final broadcast (BP flooding is VALU-bound)
+  const int base = lane & ~7;
+  double P = __shfl(th, base, 64);
 #pragma unroll
-  for (int s = 1; s < DC; ++s) {
-    const double x = __shfl_up(acc, 1, 8);
-    if (k == s) acc = x * th;
-  }
-  const double P = __shfl(acc, (lane & ~7) + DC - 1, 64);
+  for (int s = 1; s < DC; ++s) P = P * __shfl(th, base + s, 64);
   // parity of the hard decisions of the posteriors this check read (:283-285)
   const uint64_t hb = ballot(ek && pj < 0.0);
   const uint32_t par = (uint32_t)__builtin_popcount((uint32_t)(hb >> (lane & 56)) & 0xffu) & 1u;

@@ -19,6 +19,14 @@ struct OsdArgs {
   const double* post;      // [count][n] posteriors behind tiepos' order (osd_block_kernel's
                            // tie-run certification), with tiepos
   int m, n, rank, order;
+  // status-2 spill (optional): a shot left to the host also copies its
+  // posterior row to spill_post[slot] and its index to spill_idx[slot],
+  // slot = atomicAdd(spill_count, 1) (< spill_cap), so the host can fetch
+  // exactly those rows with one DMA copy, no gather kernel
+  double* spill_post;      // [spill_cap][n]
+  int32_t* spill_idx;      // [spill_cap] shot index within the call
+  int32_t* spill_count;    // [1]
+  long long spill_cap, shot_base;
   unsigned long long* prof; // QLDPC_OSD_TIMING builds only: per-phase cycle sums
   int redo;                // osd_kernel only: process just the shots whose status is 3
                            // (left by osd_block_kernel: syndrome outside H's column space)

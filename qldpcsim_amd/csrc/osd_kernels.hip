@@ -45,6 +45,20 @@ __device__ __forceinline__ uint64_t order_key(double x) {
   return __builtin_bit_cast(uint64_t, rel) - 0x3FE0000000000000ull;   // bits of 0.5
 }
 
+// a status-2 shot's posterior row into the spill buffer (OsdArgs), whole
+// workgroup; `slot` is an LDS int the block may overwrite
+__device__ __forceinline__ void spill_shot(const OsdArgs& a, long long shot, int n, int* slot) {
+  if (!a.spill_count) return;
+  if (threadIdx.x == 0) *slot = atomicAdd(a.spill_count, 1);
+  __syncthreads();
+  const long long q = *slot;
+  if (q >= a.spill_cap) return;
+  const double* src = a.post + shot * (long long)n;
+  double* dst = a.spill_post + q * (long long)n;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+  if (threadIdx.x == 0) a.spill_idx[q] = (int32_t)(a.shot_base + shot);
+}
+
 #ifndef QLDPC_OSD_TIMING
 #define QLDPC_OSD_TIMING 0  // diagnostic builds: osd_block_kernel sums per-phase cycles into a.prof
 #endif
@@ -198,6 +212,7 @@ __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
     __syncthreads();
     if (misc[3]) {
       if (t == 0) a.status[shot] = 2;
+      spill_shot(a, shot, n, slots);
       return;
     }
   }
@@ -640,6 +655,7 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
     __syncthreads();
     if (misc[5]) {
       if (t == 0) a.status[shot] = 2;
+      spill_shot(a, shot, n, misc + 7);
       return;
     }
   }

@@ -203,6 +203,14 @@ def osd_perms(post, nthreads=None):
 
 
 _POOL = {}
+_SIDE = {}
+
+
+def _side_stream(dev):
+    import torch
+    if dev.index not in _SIDE:
+        _SIDE[dev.index] = torch.cuda.Stream(dev)
+    return _SIDE[dev.index]
 
 
 def _thread_pool(n):
@@ -294,19 +302,52 @@ def osd_device_stage(items, stream=None, slot0=0, order=0):
         cs = torch.cuda.current_stream(dev)
         st = stream if stream is not None else cs.cuda_stream
         status_h = _pinned(("status", slot0 + slot), (k,), torch.int32)
-        if n <= 2048 and k >= _device_order_min() and not _host_order_only():
+        on_dev = n <= 2048 and k >= _device_order_min() and not _host_order_only()
+        spill = None
+        if on_dev:
             perm = torch.empty((k, n), dtype=torch.int32, device=dev)
             tie = torch.empty(k, dtype=torch.int32, device=dev)
-            _lib.check(_lib.lib.qldpc_osd_device_ordered(code.handle, k, syn_b.data_ptr(), post_b.data_ptr(),
-                                                         int(order), e_b.data_ptr(), status.data_ptr(),
-                                                         perm.data_ptr(), tie.data_ptr(), st))
+            # the shots left to NumPy's order copy their posteriors into a
+            # spill buffer (one DMA copy for the host later, no gather kernel)
+            cap = k // 2 + 1024
+            sp_post = _device_buf(("spill_post", slot0 + slot), (cap, n), torch.float64, dev)
+            sp_idx = _device_buf(("spill_idx", slot0 + slot), (cap,), torch.int32, dev)
+            sp_cnt = _device_buf(("spill_cnt", slot0 + slot), (1,), torch.int32, dev)
+            sp_cnt.zero_()
+            _lib.check(_lib.lib.qldpc_osd_device_ordered_ex(
+                code.handle, k, syn_b.data_ptr(), post_b.data_ptr(), int(order), e_b.data_ptr(),
+                status.data_ptr(), perm.data_ptr(), tie.data_ptr(), sp_post.data_ptr(), sp_idx.data_ptr(),
+                sp_cnt.data_ptr(), cap, st))
+            cnt_h = _pinned(("spill_cnt", slot0 + slot), (1,), torch.int32)
+            cnt_h.copy_(sp_cnt, non_blocking=True)
+            spill = (sp_post, sp_idx, cnt_h, cap)
         else:
             status.fill_(2)                            # every shot takes NumPy's order
         status_h.copy_(status, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(cs)
-        staged.append((bad, post_b, syn_b, e_b, status, status_h, ev, slot0 + slot))
+        staged.append((bad, post_b, syn_b, e_b, status, status_h, ev, slot0 + slot, on_dev, spill))
     return staged
+
+
+def osd_staged_on_device(staged):
+    """Whether osd_device_stage queued any decode's shots with the device
+    reliability order (rather than leaving them all to NumPy's)."""
+    return any(sg is not None and sg[8] for sg in staged)
+
+
+_DEVBUF = {}
+
+
+def _device_buf(key, shape, dtype, dev):
+    """Grow-only device workspaces reused across batches (per pipeline slot)."""
+    import torch
+    need = int(np.prod(shape))
+    buf = _DEVBUF.get(key)
+    if buf is None or buf.numel() < need or buf.dtype != dtype or buf.device != dev:
+        buf = torch.empty(max(need, 1), dtype=dtype, device=dev)
+        _DEVBUF[key] = buf
+    return buf[:need].view(shape)
 
 
 def osd_device_finish(items, staged, order, stream=None):
@@ -320,17 +361,36 @@ def osd_device_finish(items, staged, order, stream=None):
     for (H, syn, res), sg in zip(items, staged):
         if sg is None:
             continue
-        bad, post_b, syn_b, e_b, status, status_h, ev, slot = sg
+        bad, post_b, syn_b, e_b, status, status_h, ev, slot, _, spill = sg
         dev = res.ehat.device
         code = _lib.code_for(H, dev.index)
         ev.synchronize()
         redo = (status_h.numpy() == 2).nonzero()[0]
         res.osd_host_order = int(redo.size)
         if redo.size:
-            idx = torch.as_tensor(redo, device=dev)
             k2 = int(redo.size)
             host = _pinned(("post", slot), (k2, post_b.shape[1]), torch.float64)
-            host.copy_(post_b.index_select(0, idx))          # synchronous: needed right away
+            # fetch these posteriors with copies that wait only for this
+            # decode's OSD (its event), on a side stream, so the launch stream's
+            # next batch (decode, device OSD) runs during the host's NumPy order
+            side = _side_stream(dev)
+            side.wait_event(ev)
+            if spill is not None and k2 <= spill[3] and int(spill[2][0]) == k2:
+                # the kernels spilled exactly these rows: one contiguous DMA
+                # copy (no gather kernel waiting for free CUs behind other work)
+                sp_post, sp_idx, _, _ = spill
+                idx_h = _pinned(("spill_idx", slot), (k2,), torch.int32)
+                with torch.cuda.stream(side):
+                    host.copy_(sp_post[:k2], non_blocking=True)
+                    idx_h.copy_(sp_idx[:k2], non_blocking=True)
+                side.synchronize()
+                redo = idx_h.numpy().astype(np.int64)
+            else:
+                with torch.cuda.stream(side):
+                    idx_s = torch.as_tensor(redo, device=dev)
+                    host.copy_(post_b.index_select(0, idx_s), non_blocking=True)
+                side.synchronize()
+            idx = torch.as_tensor(redo, device=dev)
             perm_h = _pinned(("perm", slot), (k2, post_b.shape[1]), torch.int32)
             perm_h.numpy()[...] = osd_perms(host.numpy())
             perms = perm_h.to(dev, non_blocking=True)
@@ -347,13 +407,26 @@ def osd_device_finish(items, staged, order, stream=None):
     return staged
 
 
-def osd_status_check(items):
+def osd_status_check(items, defer=None):
     """Raise the reference's IndexError if any OSD of these decodes ran its
-    greedy basis loop past the last column (decoders.py:333-342)."""
+    greedy basis loop past the last column (decoders.py:333-342). With a
+    `defer` list, the per-decode flags are appended there as device tensors
+    instead (no sync; the caller checks them with osd_status_raise)."""
     for _, _, res in items:
         st = getattr(res, "osd_status", None)
-        if st is not None and bool((st != 0).any()):
+        if st is None:
+            continue
+        if defer is not None:
+            defer.append((st != 0).any())
+        elif bool((st != 0).any()):
             raise IndexError("OSD: column basis search ran past the last column")
+
+
+def osd_status_raise(flags):
+    """osd_status_check's deferred flags: one sync for all of them."""
+    import torch
+    if flags and bool(torch.stack(flags).any()):
+        raise IndexError("OSD: column basis search ran past the last column")
 
 
 def apply_osd(H, syn, ehat, post, flags, order, nthreads=0):

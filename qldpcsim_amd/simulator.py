@@ -278,12 +278,15 @@ def simulate_p(Hx: np.ndarray, Hz: np.ndarray, p: float, shots: int = 1000, decT
         ch = DeviceChannel(Hx, Hz, dev, np.random.SeedSequence(seed).generate_state(1, np.uint64)[0])
     if use_dev:
         # Two-stage pipeline over batches: the host computes batch b-1's OSD
-        # reliability orders (NumPy) while the GPU samples and decodes batch b;
+        # reliability orders (NumPy, the shots the device order leaves) while
+        # the GPU runs batch b's decode and device OSD;
         # counters accumulate on the device (one sync per batch, in the OSD
         # staging; none without OSD until the end).
         acc = torch.zeros(len(COUNTER_KEYS), dtype=torch.int64, device=dev)
         pending = None
         phase = 0
+        osd_flags = []                             # IndexError flags, checked once at the end
+        stage_first = False                        # the last batch had device-ordered OSD shots
         while done < my_shots or pending is not None:
             cur = None
             if done < my_shots:
@@ -299,21 +302,33 @@ def simulate_p(Hx: np.ndarray, Hz: np.ndarray, p: float, shots: int = 1000, decT
                                            layer_ptr=lpZ, layer_rows=lrZ, ehat_bits=packed)
                 cur = [sy_z, sy_x, errX, errZ, rX, rZ, None]
                 done += B
+            if cur is not None and osd >= 0 and stage_first:
+                # many OSD shots: this batch's device OSD is queued first
+                # (staging waits for its decode), so the GPU runs it while the
+                # host finishes the previous batch's NumPy orders below
+                cur[6] = decoders.osd_device_stage([(Hz, cur[0], cur[4]), (Hx, cur[1], cur[5])],
+                                                   slot0=2 * phase, order=osd)
+                phase ^= 1
             if pending is not None:
                 sy_z_, sy_x_, errX_, errZ_, rX_, rZ_, staged = pending
                 items = [(Hz, sy_z_, rX_), (Hx, sy_x_, rZ_)]
                 if osd >= 0:                           # (decoders.py:179-180), on the GPU
                     decoders.osd_device_finish(items, staged, osd)
-                    decoders.osd_status_check(items)
+                    decoders.osd_status_check(items, defer=osd_flags)
                 ch.count_device(sy_z_, sy_x_, errX_, errZ_, rX_.ehat, rZ_.ehat, rX_.iters, rZ_.iters, acc)
-            if cur is not None and osd >= 0:
+            if cur is not None and osd >= 0 and cur[6] is None:
+                # few OSD shots: the host's orders for the previous batch ran
+                # during this batch's decode; stage (and sync on) it now
                 cur[6] = decoders.osd_device_stage([(Hz, cur[0], cur[4]), (Hx, cur[1], cur[5])],
                                                    slot0=2 * phase, order=osd)
                 phase ^= 1
+            if cur is not None and osd >= 0:
+                stage_first = decoders.osd_staged_on_device(cur[6])
             pending = cur
             if verbose and rank == 0 and cur is not None:
                 print(f"\r(p={p:5.2e}) Decoding block n. {done:3}/{my_shots:4}... "
                       f"({done / (time.time() - t0):.3g} shots/s)", end="", flush=True)
+        decoders.osd_status_raise(osd_flags)
         tot = dict(zip(COUNTER_KEYS, (int(x) for x in acc.cpu().tolist())))
     while not use_dev and done < my_shots:
         B = min(batch_size, my_shots - done)

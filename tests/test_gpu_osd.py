@@ -253,3 +253,46 @@ def test_ordered_device_osd_tie_runs(code, order):
     np.testing.assert_array_equal(got[~ok], e[~ok])
     # the run test certifies shots whose order has ties well inside the prefix
     assert (ok & (tie < H.shape[1] // 2)).sum() > 0
+
+
+def test_ordered_osd_spill_matches_status():
+    """qldpc_osd_device_ordered_ex: every status-2 shot (and only those) spills
+    its posterior row and index; results equal the plain ordered call."""
+    import torch
+    from qldpcsim_amd import _lib
+    H, syn, e, post = _decoded_posteriors("LP118_2", 0.1, 600, 30, 21)
+    q = post.copy()
+    q[::2] = np.round(q[::2] * 2) / 2                           # many shots left to the host
+    k, n = q.shape
+    code_h = _lib.code_for(H, 0)
+    d = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a, dt), device="cuda")  # noqa: E731
+    outs = []
+    for spill in (False, True):
+        s_d, p_d, e_d = d(syn, np.uint8), d(q, np.float64), d(e, np.uint8)
+        st = torch.empty(k, dtype=torch.int32, device="cuda")
+        perm = torch.empty((k, n), dtype=torch.int32, device="cuda")
+        tie = torch.empty(k, dtype=torch.int32, device="cuda")
+        if spill:
+            cap = k
+            sp_post = torch.full((cap, n), np.nan, dtype=torch.float64, device="cuda")
+            sp_idx = torch.full((cap,), -1, dtype=torch.int32, device="cuda")
+            sp_cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+            _lib.check(_lib.lib.qldpc_osd_device_ordered_ex(
+                code_h.handle, k, s_d.data_ptr(), p_d.data_ptr(), 0, e_d.data_ptr(), st.data_ptr(),
+                perm.data_ptr(), tie.data_ptr(), sp_post.data_ptr(), sp_idx.data_ptr(), sp_cnt.data_ptr(), cap,
+                None))
+        else:
+            _lib.check(_lib.lib.qldpc_osd_device_ordered(
+                code_h.handle, k, s_d.data_ptr(), p_d.data_ptr(), 0, e_d.data_ptr(), st.data_ptr(),
+                perm.data_ptr(), tie.data_ptr(), None))
+        torch.cuda.synchronize()
+        outs.append((e_d.cpu().numpy(), st.cpu().numpy()))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    status = outs[1][1]
+    c = int(sp_cnt.item())
+    two = np.flatnonzero(status == 2)
+    assert c == two.size > 0
+    idx = sp_idx[:c].cpu().numpy()
+    assert sorted(idx.tolist()) == two.tolist()
+    np.testing.assert_array_equal(sp_post[:c].cpu().numpy(), q[idx])
