@@ -405,9 +405,11 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
       // one lane per check for long layers, a lane group when the layer leaves
       // most of the wave idle (rows <= 8: 8 lanes, <= 16: 4)
       s->layer_g = -2;
+      int g2_rows = 16;   // rows in (16, g2_rows]: 2 lanes per check
+      if (const char* ev = getenv("QLDPC_MS_G2_ROWS")) g2_rows = atoi(ev);
       for (int l = 0; l < n_layers; ++l) {
         const int rows = lay_ptr[l + 1] - lay_ptr[l];
-        const int gl = rows <= 8 ? 3 : (rows <= 16 ? 2 : 0);
+        const int gl = rows <= 8 ? 3 : (rows <= 16 ? 2 : (rows <= g2_rows ? 1 : 0));
         adj_dmax[l] = (uint8_t)(adj_dmax[l] | (gl << 5));
         s->layer_g = (s->layer_g == -2 || s->layer_g == (1 << gl)) ? (1 << gl) : 0;
       }
