@@ -1,6 +1,6 @@
 """Interleaved A/B of an environment switch on one config (same box, same process per run).
 usage: python tools/ab_env.py ENVVAR[=VALUE] code algo sched p max_iter batch [rounds]
-("on" sets ENVVAR to VALUE, default 1)"""
+("on" sets ENVVAR to VALUE, default 1; ENVVAR=ON/OFF sets OFF for "off" instead of unsetting)"""
 import json
 import os
 import subprocess
@@ -9,6 +9,7 @@ import sys
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 env_var, code, algo, sched, p, it, B = sys.argv[1:8]
 env_var, _, env_val = env_var.partition("=")
+env_val, _, env_off = env_val.partition("/")      # VAR=ON/OFF: "off" sets OFF instead of unsetting
 rounds = int(sys.argv[8]) if len(sys.argv) > 8 else 3
 snippet = (f"import sys; sys.path.insert(0, {ROOT!r}); sys.path.insert(0, {ROOT + '/tools'!r});"
            f"import bench_configs as b, json; print(json.dumps(b.run({code!r}, {algo!r}, {sched!r}, "
@@ -19,6 +20,10 @@ for r in range(rounds):
         env = dict(os.environ)
         if k == "on":
             env[env_var] = env_val or "1"
+        elif env_off:
+            env[env_var] = env_off
+        else:
+            env.pop(env_var, None)
         out = subprocess.run([sys.executable, "-c", snippet], env=env, capture_output=True, text=True)
         line = [l for l in out.stdout.splitlines() if l.startswith("{")]
         if not line:
