@@ -241,7 +241,6 @@ struct LaunchCfg {
   const void* kernel = nullptr;
   int waves = 0, blocks_per_cu = 0, lds = 0, wave_bytes = 0;
   bool lblob = false;  // uses the layer-ordered blob (ms_layered_kernel)
-  bool rec = false;    // ms_layered_rec_kernel: record blob, per-check message state
   bool gtab = false;     // ms_flood_kernel: global tables, LDS = wave state only
   int team = 0;          // bp_team_kernel: waves per half-shot (one workgroup), 0 = wave kernels
   int nh = 1;            // ms_layered_grp_kernel: half-shots per wave
@@ -262,11 +261,6 @@ struct qldpc_schedule {
   unsigned char* d_lblob = nullptr;
   int l_off_ltab = 0, l_off_lrow = 0, l_off_lay_ptr = 0, l_off_adj_ptr = 0, l_off_adj_vars = 0,
       l_off_adj_info = 0, l_off_adj_dmax = 0, l_off_vn_chk = 0;
-  // the same schedule for ms_layered_rec_kernel (check-record message state)
-  std::vector<uint8_t> rblob;
-  unsigned char* d_rblob = nullptr;
-  int r_off_ltab = 0, r_off_lrow = 0, r_off_lay_ptr = 0, r_off_adj_ptr = 0, r_off_adj_info = 0,
-      r_off_adj_dmax = 0, r_off_avar = 0, r_off_vn_edge = 0;
   int off_cn_tab = 0, off_row_ptr = 0, off_vn_ptr = 0, off_vn_chk = 0;
   int off_lay_ptr = 0, off_lay_rows = 0, off_adj_ptr = 0, off_adj_vars = 0, off_chunk_dmax = 0;
   unsigned char* d_blob = nullptr;
@@ -284,7 +278,6 @@ struct qldpc_schedule {
 };
 
 static int align16(int x) { return (x + 15) & ~15; }
-
 
 // Uniform row degree 7 or 8 with LDS offsets that fit 16 bits -> the
 // unrolled kernel instantiation and its pre-scaled table format.
@@ -428,29 +421,6 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
       s->l_off_adj_dmax = put(s->lblob, adj_dmax);
       s->l_off_vn_chk = put(s->lblob, code->avar);   // filter word per relabeled variable
       s->lblob.resize(align16((int)s->lblob.size() + 1));
-      if (m < 8192) {
-        // ms_layered_rec_kernel: rows as 16-bit colS byte offsets (no per-edge
-        // message slots), and per CSC position the (check, slot) of its edge
-        std::vector<uint16_t> ltab16((size_t)8 * lay_rows.size(), 0), vn_edge(code->E + 8, 0);
-        for (size_t q = 0; q < lay_rows.size(); ++q) {
-          const int r = lay_rows[q];
-          for (int e = code->row_ptr[r], k = 0; e < code->row_ptr[r + 1]; ++e, ++k)
-            ltab16[8 * q + k] = (uint16_t)(4 * code->vinv[code->col_idx[e]]);
-        }
-        for (int p = 0; p < code->E; ++p) {
-          const int r = vn_chk[p], k = code->csc_edge[p] - code->row_ptr[r];
-          vn_edge[p] = (uint16_t)((r << 3) | k);
-        }
-        s->r_off_ltab = put(s->rblob, ltab16);
-        s->r_off_lrow = put(s->rblob, lay_rows);
-        s->r_off_lay_ptr = put(s->rblob, lay_ptr);
-        s->r_off_adj_ptr = put(s->rblob, adj_ptr);
-        s->r_off_adj_info = put(s->rblob, adj_info);
-        s->r_off_adj_dmax = put(s->rblob, adj_dmax);
-        s->r_off_avar = put(s->rblob, code->avar);
-        s->r_off_vn_edge = put(s->rblob, vn_edge);
-        s->rblob.resize(align16((int)s->rblob.size() + 1));
-      }
     }
   }
   if (!s->layered && fast_table_ok(code) && m <= 8 * 64) {
@@ -506,10 +476,6 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
     e1 = hipMalloc(&s->d_lblob, s->lblob.size());
     if (e1 == hipSuccess) e1 = hipMemcpy(s->d_lblob, s->lblob.data(), s->lblob.size(), hipMemcpyHostToDevice);
   }
-  if (e1 == hipSuccess && !s->rblob.empty()) {
-    e1 = hipMalloc(&s->d_rblob, s->rblob.size());
-    if (e1 == hipSuccess) e1 = hipMemcpy(s->d_rblob, s->rblob.data(), s->rblob.size(), hipMemcpyHostToDevice);
-  }
   if (e1 != hipSuccess) {
     delete s;
     return fail(QLDPC_EHIP, "uploading the schedule failed: %s", hipGetErrorString(e1));
@@ -522,7 +488,6 @@ extern "C" int qldpc_schedule_destroy(qldpc_schedule* s) {
   if (!s) return QLDPC_OK;
   (void)hipFree(s->d_blob);
   (void)hipFree(s->d_lblob);
-  (void)hipFree(s->d_rblob);
   (void)hipFree(s->d_fblob);
   (void)hipFree(s->d_queue);
   delete s;
@@ -541,18 +506,6 @@ static void wave_layout(const qldpc_code* c, bool layered, int algo, int* bytes,
   *off_parw = off;
   if (layered && !colsum_f32) off = align16(off + 4 * words);  // ms_layered_kernel: filters, no parity words
   *bytes = std::max(off, 16);
-}
-
-// ms_layered_rec_kernel's slice: colS f32[n] | rec u64[m] | msk u32[m] | syn words
-static void rec_layout(const qldpc_code* c, int* bytes, int* off_rec, int* off_synw, int* off_msk) {
-  int off = align16(4 * c->n);
-  *off_rec = off;
-  off = align16(off + 8 * c->m);
-  *off_msk = off;
-  off = align16(off + 4 * c->m);
-  *off_synw = off;
-  off = align16(off + 4 * 2 * ((c->m + 63) / 64));
-  *bytes = off;
 }
 
 // ms_layered_grp_kernel's per-half-shot slice: colS f32[n] | c2v f32[E + 8] | syndrome u8[m]
@@ -619,16 +572,6 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
       cfg.kernel = qldpc::select_ms_layered_grp_kernel(dc, nh, gg, &cfg.name);
       if (cfg.kernel) cfg.nh = nh;
     }
-    if (!cfg.kernel && !s->rblob.empty()) {
-      // per-check message records (ms_layered_rec_kernel) where per-edge
-      // state limits the waves per CU by LDS
-      // (opt-in: measured 1.5-1.9x slower than per-edge state)
-      const char* ev = getenv("QLDPC_MS_REC");
-      if (ev && atoi(ev) != 0) {
-        cfg.kernel = qldpc::select_ms_layered_rec_kernel(dc, g, &cfg.name);
-        cfg.rec = cfg.kernel != nullptr;
-      }
-    }
     if (!cfg.kernel) cfg.kernel = qldpc::select_ms_layered_kernel(dc, g, &cfg.name);
     use_lblob = cfg.kernel != nullptr;
   }
@@ -650,7 +593,6 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   int off_c2v, off_synw, off_parw, off_red;
   wave_layout(c, s->layered, algo, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw, use_lblob);
   if (team) team_layout(c, team, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw, &off_red);
-  if (cfg.rec) rec_layout(c, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw);
   if (cfg.nh > 1 || (use_lblob && cfg.name && strstr(cfg.name, "grp"))) {
     grp_layout(c, &cfg.slice, &off_c2v, &off_synw);
     cfg.wave_bytes = cfg.nh * cfg.slice;
@@ -659,8 +601,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   HIP_TRY(hipGetDevice(&dev));
   HIP_TRY(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
   HIP_TRY(qldpc::configure_kernel(cfg.kernel, max_lds));
-  const int blob = gtab ? QLDPC_FLOOD_HDR
-                        : (int)(cfg.rec ? s->rblob.size() : (use_lblob ? s->lblob.size() : s->blob.size()));
+  const int blob = gtab ? QLDPC_FLOOD_HDR : (int)(use_lblob ? s->lblob.size() : s->blob.size());
   int best_waves = 0;
   if (team) {  // one team (workgroup of `team` waves) per half-shot
     const int lds = blob + cfg.wave_bytes;
@@ -819,19 +760,6 @@ extern "C" int qldpc_decode_device_ex(const qldpc_code* code, const qldpc_schedu
     a.off_row_ptr = sched->l_off_adj_info;
     a.off_chunk_dmax = sched->l_off_adj_dmax;
     a.off_vn_chk = sched->l_off_vn_chk;
-  }
-  if (cfg->rec) {  // ms_layered_rec_kernel's blob and slice
-    a.blob = sched->d_rblob;
-    a.blob_bytes = (int)sched->rblob.size();
-    a.off_cn_tab = sched->r_off_ltab;
-    a.off_lay_rows = sched->r_off_lrow;
-    a.off_lay_ptr = sched->r_off_lay_ptr;
-    a.off_adj_ptr = sched->r_off_adj_ptr;
-    a.off_row_ptr = sched->r_off_adj_info;
-    a.off_chunk_dmax = sched->r_off_adj_dmax;
-    a.off_vn_chk = sched->r_off_avar;
-    a.off_adj_vars = sched->r_off_vn_edge;
-    rec_layout(code, &a.wave_bytes, &a.off_c2v, &a.off_synw, &a.off_parw);
   }
   if (cfg->team) team_layout(code, cfg->team, &a.wave_bytes, &a.off_c2v, &a.off_synw, &a.off_parw, &a.off_red);
   if (cfg->slice) grp_layout(code, &a.wave_bytes, &a.off_c2v, &a.off_synw);   // per half-shot slice

@@ -1419,301 +1419,6 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
 }
 
 // ---------------------------------------------------------------------------
-// Layered MS with the check-to-variable state held per CHECK ("records")
-// instead of per edge. decoders.py:160-168 gives every edge of a check one of
-// two magnitudes and its own sign, so check c's messages are
-//   rec[c] = (c1n, c2n)  fl32(beta*min1), fl32(beta*min2) as float32 bit
-//                        patterns with the check's sign (syndrome x sign
-//                        product) folded in
-//   msk[c]  bit k        edge k took min2 (|v_k| == min1)
-//           bit 8 + k    sign of v_k
-// and edge k's message is (bit k ? c2n : c1n) ^ (bit 8+k) << 31: the float
-// ms_layered_kernel stores, bit for bit. 12 B per check instead of 4 B per
-// edge (LP118_2: 5.4 KB instead of 14.4 KB per half-shot), so a code whose
-// per-edge state bounds the waves per CU by LDS runs about twice as many; the
-// variable node pays a table hop (vn_edge: check and slot of each CSC
-// position) and a decode per edge.
-// Blob (capi.cpp, rblob): ltab16 [Q][8] u16 = 4 * relabeled variable (byte
-// offset into colS), lrow, lay_ptr, adj_ptr, adj_info and adj_dmax as
-// ms_layered_kernel, avar, vn_edge [E + 8] u16 = check << 3 | slot.
-// Slice: colS f32[n] | rec u64[m] (off_c2v) | msk u32[m] (off_parw) |
-// syndrome words (off_synw).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t rec_msg_bits(uint64_t r, uint32_t mk, uint32_t k) {
-  const uint32_t base = ((mk >> k) & 1u) ? (uint32_t)(r >> 32) : (uint32_t)r;
-  return base ^ ((mk << (23u - k)) & 0x80000000u);
-}
-
-template <int DC, int G>
-__device__ __forceinline__ void cn_rec(const DecodeArgs& a, const uint16_t* trow, int sub, bool live,
-                                       uint32_t synb, bool first, uint32_t cols_b, uint32_t rec_a,
-                                       uint32_t msk_a, int& fl) {
-  constexpr int EPL = 8 / G;
-  uint32_t t[EPL];
-  if constexpr (EPL == 8) {
-    const uint4 w = *(const uint4*)trow;
-    const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      t[2 * i] = ww[i] & 0xffffu;
-      t[2 * i + 1] = ww[i] >> 16;
-    }
-  } else if constexpr (EPL == 4) {
-    const uint2 w = *(const uint2*)(trow + 4 * sub);
-    t[0] = w.x & 0xffffu; t[1] = w.x >> 16; t[2] = w.y & 0xffffu; t[3] = w.y >> 16;
-  } else if constexpr (EPL == 2) {
-    const uint32_t w = *(const uint32_t*)(trow + 2 * sub);
-    t[0] = w & 0xffffu; t[1] = w >> 16;
-  } else {
-    t[0] = trow[sub];
-  }
-  bool ek[EPL];
-#pragma unroll
-  for (int i = 0; i < EPL; ++i) ek[i] = live && (DC == 8 || EPL * sub + i < DC);
-  uint64_t r = 0;
-  uint32_t mk = 0;
-  if (!first) {
-    r = *QLDPC_LDS(const uint64_t, rec_a);
-    mk = *QLDPC_LDS(const uint32_t, msk_a);
-  }
-  const uint32_t mks = mk >> (EPL * sub);                         // this lane's slots at bits i, 8 + i
-  double v[EPL];
-  uint32_t hv[EPL];
-#pragma unroll
-  for (int i = 0; i < EPL; ++i) {
-    if (first) {
-      v[i] = (double)a.L32;                                       // (:148-149)
-    } else {
-      const double pj = a.L + (double)*QLDPC_LDS(const float, cols_b + t[i]);   // post (:173)
-      v[i] = pj - (double)__builtin_bit_cast(float, rec_msg_bits(r, mks, (uint32_t)i));  // v2c (:177)
-    }
-    hv[i] = ek[i] ? hi_word(v[i]) : 0u;
-  }
-  double av[EPL];
-#pragma unroll
-  for (int i = 0; i < EPL; ++i) av[i] = ek[i] ? v[i] : __builtin_inf();
-  double lo, hi;
-  min12_tree<EPL>(av, lo, hi);
-  uint32_t sh = xor_tree<EPL>(hv);                                // np.sign product (:157-159)
-  if constexpr (G >= 2) group_merge<kDppQuadXor1>(lo, hi, sh);
-  if constexpr (G >= 4) group_merge<kDppQuadXor2>(lo, hi, sh);
-  if constexpr (G >= 8) group_merge<kDppHalfMirror>(lo, hi, sh);
-  double m1 = lo, m2 = hi;
-  if (__builtin_expect(ballot(live && ((lo == 0.0) | (hi == __builtin_inf()))) != 0, 0)) {
-    m1 = __builtin_isinf(lo) ? 0.0 : lo;                          // (:165)
-    m2 = __builtin_isinf(hi) ? 0.0 : hi;                          // (:166)
-    if (m1 == 0.0 && live) fl |= FLAG_MIN_ZERO;
-  }
-  const uint32_t npm = ((sh >> 31) ^ synb) << 31;
-  const uint32_t c1n = __builtin_bit_cast(uint32_t, (float)(a.beta * m1)) ^ npm;
-  const uint32_t c2n = __builtin_bit_cast(uint32_t, (float)(a.beta * m2)) ^ npm;
-  uint32_t bits = 0;                                              // (:167-168) as slot bits
-#pragma unroll
-  for (int i = 0; i < EPL; ++i)
-    if (ek[i]) bits |= ((uint32_t)(__builtin_fabs(v[i]) == lo) << i) | ((hv[i] >> 31) << (8 + i));
-  bits <<= EPL * sub;
-  if constexpr (G >= 2) bits |= dpp_u32<kDppQuadXor1>(bits);
-  if constexpr (G >= 4) bits |= dpp_u32<kDppQuadXor2>(bits);
-  if constexpr (G >= 8) bits |= dpp_u32<kDppHalfMirror>(bits);
-  if (live && sub == 0) {
-    *QLDPC_LDS(uint64_t, rec_a) = ((uint64_t)c2n << 32) | c1n;
-    *QLDPC_LDS(uint32_t, msk_a) = bits;
-  }
-}
-
-// Variable node of one layer from the records: as vn_layer, with each c2v
-// read as (vn_edge -> record + mask -> decode).
-template <int K>
-__device__ __forceinline__ uint32_t vn_layer_rec(const uint32_t* adj_info, const uint32_t* avar,
-                                                 const uint16_t* vn_edge, float* colS, uint32_t rec_b,
-                                                 uint32_t msk_b, int v0, int v1, int lane, float thr) {
-  uint32_t acc = 0;
-  for (int qb = v0; qb < v1; qb += 128) {
-    uint32_t info[2];
-    bool in[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int q = qb + 64 * h + lane;
-      in[h] = q < v1;
-      info[h] = adj_info[in[h] ? q : v0];
-    }
-    float old[2];
-    uint32_t av[2], e[2][K];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      old[h] = colS[info[h] >> 21];
-      av[h] = avar[info[h] >> 21];
-      const uint16_t* ve = vn_edge + (info[h] & 0xffffu);
-#pragma unroll
-      for (int t = 0; t < K; ++t) e[h][t] = ve[t];                // vn_edge padded by 8 entries
-    }
-    uint64_t r[2][K];
-    uint32_t mk[2][K];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int t = 0; t < K; ++t) {
-        const uint32_t c8 = e[h][t] & ~7u;                        // 8 * check
-        r[h][t] = *QLDPC_LDS(const uint64_t, rec_b + c8);
-        mk[h][t] = *QLDPC_LDS(const uint32_t, msk_b + (c8 >> 1));
-      }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int d = (int)((info[h] >> 16) & 31u);
-      float s = 0.0f;                                             // sequential, ascending check (:172)
-#pragma unroll
-      for (int t = 0; t < K; ++t) {
-        const float x = __builtin_bit_cast(float, rec_msg_bits(r[h][t], mk[h][t], e[h][t] & 7u));
-        s += (t < d) ? x : 0.0f;
-      }
-      if (in[h]) colS[info[h] >> 21] = s;
-      const bool flip = in[h] && ((old[h] < thr) != (s < thr));   // hard decision flipped (:173-174)
-      acc ^= flip ? av[h] : 0u;
-    }
-  }
-  return acc;
-}
-
-template <int DC, int GG>
-__device__ __forceinline__ void cn_layer_rec(const DecodeArgs& a, const uint16_t* ltab16, const uint16_t* lrow,
-                                             const uint32_t* synw, int q0, int q1, int lane, bool first,
-                                             uint32_t cols_b, uint32_t rec_b, uint32_t msk_b, int& fl) {
-  for (int qb = q0; qb < q1; qb += 64 / GG) {
-    const int q = qb + lane / GG;
-    const bool live = q < q1;
-    const int qs = live ? q : q0;
-    const int c = lrow[qs];
-    const uint32_t sb = (synw[c >> 5] >> (c & 31)) & 1u;
-    cn_rec<DC, GG>(a, ltab16 + qs * 8, lane & (GG - 1), live, sb, first, cols_b, rec_b + 8u * (uint32_t)c,
-                   msk_b + 4u * (uint32_t)c, fl);
-  }
-}
-
-template <int DC, int G>
-__global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_rec_kernel(DecodeArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  {
-    const uint4* src = (const uint4*)a.blob;
-    uint4* dst = (uint4*)lds;
-    const int nvec = a.blob_bytes >> 4;
-    for (int i = threadIdx.x; i < nvec; i += blockDim.x) dst[i] = src[i];
-  }
-  __syncthreads();
-  const uint16_t* ltab16 = (const uint16_t*)(lds + a.off_cn_tab);    // [Q][8]
-  const uint16_t* lrow = (const uint16_t*)(lds + a.off_lay_rows);    // [Q]
-  const uint16_t* lay_ptr = (const uint16_t*)(lds + a.off_lay_ptr);  // [L+1]
-  const uint16_t* adj_ptr = (const uint16_t*)(lds + a.off_adj_ptr);  // [L+1]
-  const uint32_t* adj_info = (const uint32_t*)(lds + a.off_row_ptr); // [A] var<<21 | deg<<16 | csc start
-  const uint8_t* adj_dmax = (const uint8_t*)(lds + a.off_chunk_dmax);// [L] max degree | lanes-per-check code
-  const uint32_t* avar = (const uint32_t*)(lds + a.off_vn_chk);      // [n] filter word per variable
-  const uint16_t* vn_edge = (const uint16_t*)(lds + a.off_adj_vars); // [E+8] check << 3 | slot
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  const int waves = blockDim.x >> 6;
-  unsigned char* ws = lds + a.blob_bytes + wid * a.wave_bytes;
-  float* colS = (float*)ws;
-  uint64_t* rec = (uint64_t*)(ws + a.off_c2v);
-  uint32_t* msk = (uint32_t*)(ws + a.off_parw);
-  uint32_t* synw = (uint32_t*)(ws + a.off_synw);
-  const uint32_t cols_b = lds_addr(colS), rec_b = lds_addr(rec), msk_b = lds_addr(msk);
-  const int m = a.m, n = a.n;
-  const float thr = a.hd_thresh;
-  VinvRegs<16> vr;                                             // n <= 1024 in registers
-  vr.load(a.vinv, n, lane);
-
-  for (HalfShotQueue Q(a, waves, wid); Q.hs < a.batch; Q.advance()) {
-    const long long hs = Q.hs;
-    Q.prefetch(threadIdx.x & 63);
-    int fl = 0;
-    int iters = a.max_iter;
-    bool conv = false;
-    const double L = a.L;
-    load_syndrome_bits<8>(a, hs, synw, lane);
-    for (int j = lane; j < n; j += 64) colS[j] = 0.0f;          // post = L, c2v = 0 (:148-150)
-    for (int c = lane; c < m; c += 64) {
-      rec[c] = 0ull;
-      msk[c] = 0u;
-    }
-    wave_sync();
-    uint32_t bl = 0;                                           // filter parities (ms_layered_kernel)
-    for (int c = lane; c < m; c += 64) bl ^= ((synw[c >> 5] >> (c & 31)) & 1u) ? a.wc[c] : 0u;
-    const uint32_t B = wave_xor(bl);
-    uint32_t F = (L < 0.0) ? a.filt_all : 0u;
-    bool first = true;
-    for (int it = 0; it < a.max_iter && !conv; ++it) {
-      for (int l = 0; l < a.n_layers; ++l) {
-        const int q0 = lay_ptr[l], q1 = lay_ptr[l + 1];
-        if constexpr (G != 0) {
-          cn_layer_rec<DC, G>(a, ltab16, lrow, synw, q0, q1, lane, first, cols_b, rec_b, msk_b, fl);
-        } else {
-          switch (__builtin_amdgcn_readfirstlane((int)adj_dmax[l]) >> 5) {
-            case 0: cn_layer_rec<DC, 1>(a, ltab16, lrow, synw, q0, q1, lane, first, cols_b, rec_b, msk_b, fl); break;
-            case 1: cn_layer_rec<DC, 2>(a, ltab16, lrow, synw, q0, q1, lane, first, cols_b, rec_b, msk_b, fl); break;
-            case 2: cn_layer_rec<DC, 4>(a, ltab16, lrow, synw, q0, q1, lane, first, cols_b, rec_b, msk_b, fl); break;
-            default: cn_layer_rec<DC, 8>(a, ltab16, lrow, synw, q0, q1, lane, first, cols_b, rec_b, msk_b, fl); break;
-          }
-        }
-        first = false;
-        wave_sync();
-        const int v0 = adj_ptr[l], v1 = adj_ptr[l + 1];
-        const int dmax = __builtin_amdgcn_readfirstlane((int)adj_dmax[l]) & 31;
-        uint32_t acc = 0;
-        switch (dmax) {
-          case 3: acc = vn_layer_rec<3>(adj_info, avar, vn_edge, colS, rec_b, msk_b, v0, v1, lane, thr); break;
-          case 4: acc = vn_layer_rec<4>(adj_info, avar, vn_edge, colS, rec_b, msk_b, v0, v1, lane, thr); break;
-          case 5: acc = vn_layer_rec<5>(adj_info, avar, vn_edge, colS, rec_b, msk_b, v0, v1, lane, thr); break;
-          case 6: acc = vn_layer_rec<6>(adj_info, avar, vn_edge, colS, rec_b, msk_b, v0, v1, lane, thr); break;
-          default:
-            for (int q = v0 + lane; q < v1; q += 64) {
-              const uint32_t info = adj_info[q];
-              const int j = (int)(info >> 21), d = (int)((info >> 16) & 31u);
-              const uint16_t* ve = vn_edge + (info & 0xffffu);
-              const float old = colS[j];
-              float s = 0.0f;
-              for (int t = 0; t < d; ++t) {
-                const uint32_t e = ve[t], c8 = e & ~7u;
-                s += __builtin_bit_cast(float, rec_msg_bits(*QLDPC_LDS(const uint64_t, rec_b + c8),
-                                                            *QLDPC_LDS(const uint32_t, msk_b + (c8 >> 1)), e & 7u));
-              }
-              colS[j] = s;
-              if ((old < thr) != (s < thr)) acc ^= avar[j];
-            }
-        }
-        F ^= wave_xor(acc);
-        wave_sync();
-        if (F == B && layered_full_check<DC>(a, colS, synw, lane, thr)) {   // stop test (:175-176)
-          iters = it + 1;
-          conv = true;
-          break;
-        }
-      }
-    }
-    {                                                          // ê, posteriors in original order
-      double* po = a.post ? a.post + hs * (long long)n : nullptr;
-      for (int k = 0; k < 16 && 64 * k < n; ++k) {
-        const int jo = 64 * k + lane;
-        if (jo < n) {
-          const double pv = L + (double)colS[n <= 1024 ? vr.get(k) : a.vinv[jo]];
-          put_ehat(a, hs, jo, pv < 0.0);
-          if (po) po[jo] = pv;
-        }
-      }
-      for (int jo = 1024 + lane; jo < n; jo += 64) {
-        const double pv = L + (double)colS[a.vinv[jo]];
-        put_ehat(a, hs, jo, pv < 0.0);
-        if (po) po[jo] = pv;
-      }
-    }
-    const uint64_t b1 = ballot((fl & FLAG_MIN_ZERO) != 0);
-    if (lane == 0) {
-      a.iters[hs] = iters;
-      if (a.flags) a.flags[hs] = (int32_t)((b1 ? FLAG_MIN_ZERO : 0) | (conv ? FLAG_CONVERGED : 0));
-    }
-    wave_sync();
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Layered / serial min-sum with NH half-shots per wavefront (LPH = 64 / NH
 // lanes each). Layers are short (LP118_0: 16 / 32 rows, 128-208 adjacent
 // variables), so with one half-shot per wave most lanes idle in the check
@@ -2258,14 +1963,6 @@ const void* select_ms_layered_kernel(int dc, int g, const char** name) {
   QLDPC_MSL(7, 0) QLDPC_MSL(8, 0) QLDPC_MSL(7, 1) QLDPC_MSL(8, 1) QLDPC_MSL(7, 2) QLDPC_MSL(8, 2)
   QLDPC_MSL(7, 4) QLDPC_MSL(8, 4) QLDPC_MSL(7, 8) QLDPC_MSL(8, 8)
 #undef QLDPC_MSL
-  return nullptr;
-}
-
-const void* select_ms_layered_rec_kernel(int dc, int g, const char** name) {
-#define QLDPC_MSR(D, Gn) if (dc == D && g == Gn) QLDPC_NAMED((&ms_layered_rec_kernel<D, Gn>), "ms_layered_rec_kernel<" #D ", " #Gn ">");
-  QLDPC_MSR(7, 0) QLDPC_MSR(8, 0) QLDPC_MSR(7, 1) QLDPC_MSR(8, 1) QLDPC_MSR(7, 2) QLDPC_MSR(8, 2)
-  QLDPC_MSR(7, 4) QLDPC_MSR(8, 4) QLDPC_MSR(7, 8) QLDPC_MSR(8, 8)
-#undef QLDPC_MSR
   return nullptr;
 }
 

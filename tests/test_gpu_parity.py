@@ -226,8 +226,7 @@ def test_decode_batch_into_preallocated_buffers(dec):
 
 
 
-KERNELS = ["G1", "G2", "G4", "G8", "R0", "R1", "R2", "R4", "R8", "generic", "default",
-           "N1G4", "N2G1", "N2G2", "N4G1", "N4G2"]
+KERNELS = ["G1", "G2", "G4", "G8", "generic", "default", "N1G4", "N2G1", "N2G2", "N4G1", "N4G2"]
 
 
 @pytest.mark.parametrize("code", ["LP118_2", "LP118_0", "LP04_0"])
@@ -240,9 +239,7 @@ def test_ms_layered_kernels_match_oracle(dec, kernel, code, monkeypatch):
     (QLDPC_MS_GROUPS=1, QLDPC_MS_LANES_PER_CHECK), ms_layered_grp_kernel with
     NH half-shots per wave and G lanes per check (QLDPC_MS_GROUPS,
     QLDPC_MS_GRP_G), the default choice, and the generic decode kernel
-    (QLDPC_NO_LAYERED_FAST), and ms_layered_rec_kernel (per-check message
-    records, QLDPC_MS_REC=1) at every G and with G chosen per layer (R0).
-    Lane mappings and message storage never change the arithmetic."""
+    (QLDPC_NO_LAYERED_FAST). Lane mappings never change the arithmetic."""
     from oracle import oracle
     from qldpcsim_amd import _lib, codes, schedule
     Hx, Hz = codes.load_code(code)
@@ -250,10 +247,6 @@ def test_ms_layered_kernels_match_oracle(dec, kernel, code, monkeypatch):
         monkeypatch.setenv("QLDPC_NO_LAYERED_FAST", "1")
     elif kernel.startswith("G"):
         monkeypatch.setenv("QLDPC_MS_GROUPS", "1")
-        monkeypatch.setenv("QLDPC_MS_REC", "0")
-        monkeypatch.setenv("QLDPC_MS_LANES_PER_CHECK", kernel[1:])
-    elif kernel.startswith("R"):
-        monkeypatch.setenv("QLDPC_MS_REC", "1")
         monkeypatch.setenv("QLDPC_MS_LANES_PER_CHECK", kernel[1:])
     elif kernel.startswith("N"):
         monkeypatch.setenv("QLDPC_MS_GROUPS", kernel[1])
@@ -268,13 +261,9 @@ def test_ms_layered_kernels_match_oracle(dec, kernel, code, monkeypatch):
     code_h._sched.clear()                  # launch configs read the env once per schedule
     try:
         r = dec.decode_batch(Hz, syn, 0.06 / 3, 30, algo="MS", want_post=True, layer_ptr=lp, layer_rows=lr)
-        nm = _lib.kernel_name(Hz, lp, lr, "MS")
         if kernel.startswith("N"):
+            nm = _lib.kernel_name(Hz, lp, lr, "MS")
             assert nm.startswith("ms_layered_grp_kernel<") and nm.endswith(f", {kernel[1]}, {kernel[3:]}>"), nm
-        elif kernel.startswith("R"):
-            assert nm.startswith("ms_layered_rec_kernel<") and nm.endswith(f", {kernel[1:]}>"), nm
-        elif kernel.startswith("G"):
-            assert nm.startswith("ms_layered_kernel<") and nm.endswith(f", {kernel[1:]}>"), nm
     finally:
         code_h._sched.clear()
     e, it, post, fl = oracle.decode_batch("MS", Hz, syn, 0.06 / 3, 30, lp, lr)
@@ -313,17 +302,14 @@ def test_ms_layered_large_mixed_batch(dec, groups, monkeypatch):
     np.testing.assert_array_equal(r.post.view(np.uint64), post.view(np.uint64))
 
 
-@pytest.mark.parametrize("rec", ["0", "1"])
 @pytest.mark.parametrize("sched", ["L", "S"])
-def test_ms_layered_irregular_columns_match_oracle(dec, sched, rec, monkeypatch):
+def test_ms_layered_irregular_columns_match_oracle(dec, sched):
     """Layered / serial MS on a synthetic uniform-row-degree-8 code whose
     column degrees run from 1 to ~20 (bundled codes only have 3-5): exercises
-    the layered kernels' generic VN branch (degree bounds outside 3-6), layers
-    whose adjacency is not a multiple of 64, and heavy parity toggling; with
-    per-edge (rec 0) and per-check (rec 1, ms_layered_rec_kernel) messages."""
+    the layered kernel's generic VN branch (degree bounds outside 3-6), layers
+    whose adjacency is not a multiple of 64, and heavy parity toggling."""
     from oracle import oracle
-    from qldpcsim_amd import _lib, schedule
-    monkeypatch.setenv("QLDPC_MS_REC", rec)
+    from qldpcsim_amd import schedule
     rng = np.random.default_rng(21)
     m, n = 96, 200
     H = np.zeros((m, n), np.uint8)
@@ -338,14 +324,7 @@ def test_ms_layered_irregular_columns_match_oracle(dec, sched, rec, monkeypatch)
     syn = np.concatenate([rng.integers(0, 2, (256, H.shape[0]), dtype=np.uint8),
                           ((rng.random((256, H.shape[1])) < 0.03).astype(np.int64) @ H.T.astype(np.int64) % 2)
                           .astype(np.uint8)])
-    code_h = _lib.code_for(H)
-    code_h._sched.clear()                  # launch configs read the env once per schedule
-    try:
-        assert _lib.kernel_name(H, lp, lr, "MS").startswith(
-            "ms_layered_rec_kernel<" if rec == "1" else "ms_layered_kernel<")
-        r = dec.decode_batch(H, syn, 0.05 / 3, 25, algo="MS", want_post=True, layer_ptr=lp, layer_rows=lr)
-    finally:
-        code_h._sched.clear()
+    r = dec.decode_batch(H, syn, 0.05 / 3, 25, algo="MS", want_post=True, layer_ptr=lp, layer_rows=lr)
     e, it, post, fl = oracle.decode_batch("MS", H, syn, 0.05 / 3, 25, lp, lr)
     np.testing.assert_array_equal(r.iters, it)
     np.testing.assert_array_equal(r.ehat, e)
