@@ -45,7 +45,21 @@ QLDPC_HD uint64_t qldpc_d2bits(double d) {
   return u;
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+/* v_fma_f64 with every operand in a register. Written as __builtin_fma, a
+   Horner step q = fma(q, r, c) became v_mov (copy the coefficient c into the
+   destination) + v_fmac_f64 (accumulate form, c tied to the destination):
+   two VALU ops per step in a VALU-bound kernel. Same operation, same
+   rounding. */
+__device__ __forceinline__ double qldpc_fma_dev(double a, double b, double c) {
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+#define QLDPC_FMA(a, b, c) qldpc_fma_dev((a), (b), (c))
+#else
 #define QLDPC_FMA(a, b, c) __builtin_fma((a), (b), (c))
+#endif
 
 #define QLDPC_LN2_HI 6.93147180369123816490e-01 /* 0x3fe62e42fee00000: k*LN2_HI exact for |k| < 2^11 */
 #define QLDPC_LN2_LO 1.90821492927058770002e-10 /* 0x3dea39ef35793c76 */

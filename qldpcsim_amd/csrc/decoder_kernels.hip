@@ -1751,7 +1751,7 @@ __device__ __forceinline__ uint32_t cn_bp_group(const DecodeArgs& a, const LdsVi
 }
 
 template <bool LAYERED, int DC, int W>
-__global__ void __launch_bounds__(64 * W) bp_team_kernel(DecodeArgs a) {
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) bp_team_kernel(DecodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   {
     const uint4* src = (const uint4*)a.blob;
