@@ -57,8 +57,26 @@ __device__ __forceinline__ double qldpc_fma_dev(double a, double b, double c) {
   return r;
 }
 #define QLDPC_FMA(a, b, c) qldpc_fma_dev((a), (b), (c))
+/* a / b correctly rounded, for finite b != 0 and operands whose exponents lie
+   well inside the normal range (here: 2^-500 < |a|, |b| < 2^500, or a == 0).
+   It is the compiler's IEEE division sequence (v_rcp_f64, two Newton steps,
+   q = a r, one FMA correction) without v_div_scale / v_div_fixup, which are the
+   identity in that range: the same result, bit for bit, in 8 instead of 11
+   VALU ops. Callers guarantee the range. */
+__device__ __forceinline__ double qldpc_div_dev(double a, double b) {
+  double r = __builtin_amdgcn_rcp(b);
+  double e = qldpc_fma_dev(-b, r, 1.0);
+  r = qldpc_fma_dev(r, e, r);
+  e = qldpc_fma_dev(-b, r, 1.0);
+  r = qldpc_fma_dev(r, e, r);
+  const double q = a * r;
+  const double rem = qldpc_fma_dev(-b, q, a);
+  return qldpc_fma_dev(rem, r, q);
+}
+#define QLDPC_DIV(a, b) qldpc_div_dev((a), (b))
 #else
 #define QLDPC_FMA(a, b, c) __builtin_fma((a), (b), (c))
+#define QLDPC_DIV(a, b) ((a) / (b))
 #endif
 
 #define QLDPC_LN2_HI 6.93147180369123816490e-01 /* 0x3fe62e42fee00000: k*LN2_HI exact for |k| < 2^11 */
@@ -101,7 +119,8 @@ QLDPC_HD double qldpc_tanh(double x) {
   /* branch-free (lanes diverge): the range cases are selects */
   const double ac = a < 22.0 ? a : 22.0;
   const double em = qldpc_expm1_pos(ac + ac);
-  double t = em / (em + 2.0);                     /* one division, any a (<= 3 ULP) */
+  double t = QLDPC_DIV(em, em + 2.0);             /* one division (<= 3 ULP); em + 2 in [2, 2^64],
+                                                     em = 0 or > 2^-500 where t is kept */
   t = a >= 22.0 ? 1.0 : t;                        /* 1 - tanh(22) < 2^-62 */
   t = a < 3.7252902984e-09 ? a : t;               /* 2^-28: tanh(x) = x in double */
   return qldpc_bits2d(qldpc_d2bits(t) | sgn);
@@ -205,7 +224,8 @@ QLDPC_HD double qldpc_atanh(double x) {
   const double num = (N - Dk) + (eN - eDk);         /* N - Dk exact (Sterbenz) */
   const double den = (N + Dk) + (eN + eDk);
   const int big = a > 0.17157287525381;             /* 3 - 2 sqrt2 (rounded down) */
-  const double sr = big ? num / den : a;            /* below: k = 0, s = a exactly */
+  const double sr = big ? QLDPC_DIV(num, den) : a; /* below: k = 0, s = a exactly; den in [1, 4],
+                                                     num = 0 or |num| > 2^-110 where big */
   const double fk = big ? (double)k : 0.0;
   const double t = QLDPC_FMA(fk, 0.5 * QLDPC_LN2_HI, qldpc_atanh_small(sr) + fk * (0.5 * QLDPC_LN2_LO));
   return qldpc_bits2d(qldpc_d2bits(t) | sgn);

@@ -1739,9 +1739,17 @@ __device__ __forceinline__ uint32_t cn_bp_group(const DecodeArgs& a, const LdsVi
   const uint32_t par = (uint32_t)__builtin_popcount((uint32_t)(hb >> (lane & 56)) & 0xffu) & 1u;
   if (ek) {
     if (th == 0.0) fl |= FLAG_NONFINITE;
-    double th2 = P / th;                                  // (:256)
-    if (__builtin_fabs(th2) >= 1.0 - a.eps)               // (:257-258)
-      th2 = th2 - a.eps * (th2 > 0.0 ? 1.0 : (th2 < 0.0 ? -1.0 : 0.0));
+    // P / th (:256). QLDPC_DIV is IEEE division for operands in the normal
+    // range (|th| <= 1 and |P| <= |th| here); a wave holding a zero, tiny or
+    // non-finite one divides the general way.
+    double th2;
+    if (__builtin_expect(ballot(!(__builtin_fabs(th) > 1e-150 && (P == 0.0 || __builtin_fabs(P) > 1e-150))) != 0, 0))
+      th2 = P / th;
+    else
+      th2 = QLDPC_DIV(P, th);
+    // (:257-258): |th2| >= 1 - eps implies th2 != 0, so eps * sign(th2) is
+    // copysign(eps, th2) (a NaN compares false and stays)
+    th2 = (__builtin_fabs(th2) >= 1.0 - a.eps) ? th2 - __builtin_copysign(a.eps, th2) : th2;
     double val = 2.0 * qldpc_atanh(th2);                  // (:259)
     if (synb) val = -val;                                 // (:260-261)
     if (!__builtin_isfinite(val)) fl |= FLAG_NONFINITE;
