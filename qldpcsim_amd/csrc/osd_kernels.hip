@@ -289,15 +289,17 @@ __device__ __forceinline__ uint32_t wave_or32(uint32_t x) {
 
 // Phase B over the columns `cols` of one half-word (HI: bits 32..63, read
 // from hi[]) on the first SF compact slots, straight-line per column: one
-// ballot per slot (SGPR lane masks) masked by the still-free rows, the first
-// hit by scalar selects, the pivot's values by uniform slot select +
-// readlane, the elimination under exec masks. Pivot k's compact position and
-// column bit go to pk[k]; returns the pivot count K.
+// ballot per slot masked by the slot's still-free rows (fm[s], a wave-uniform
+// lane mask in SGPRs), the first hit by scalar selects, the pivot's values by
+// a uniform switch on its slot + readlane, the elimination under exec masks.
+// Pivot k's compact position and column bit go to pk[k]; returns the pivot
+// count K.
 template <int SL, int SF, bool HI>
 __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL], uint32_t (&cl)[SL],
-                                          uint32_t (&ch)[SL], uint32_t& frv, uint32_t cols, int K,
+                                          uint32_t (&ch)[SL], uint64_t (&fm)[SL], uint32_t cols, int K,
                                           int w, int lane, int& rank, int& nJ, bool& done, uint64_t& pivm,
                                           int rankH, int m, int* pk, int* Jl, unsigned char* inJ) {
+  static_assert(SL <= 8, "the pivot-slot switch covers 8 slots");
   while (cols && !done) {
     // loop-carried scalars re-asserted wave-uniform: otherwise the compiler
     // keeps them per lane and turns the loop into an exec-masked one
@@ -316,7 +318,7 @@ __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL]
       const uint32_t bm = 1u << bit;
 #pragma unroll
       for (int s = SF - 1; s >= 0; --s) {
-        const uint64_t c = __ballot(((HI ? hi[s] : lo[s]) & bm) != 0 && ((frv >> s) & 1u));
+        const uint64_t c = __ballot(((HI ? hi[s] : lo[s]) & bm) != 0) & fm[s];
         f = c ? 64 * s + (int)__builtin_ctzll(c) : f;
       }
       f = __builtin_amdgcn_readfirstlane(f);
@@ -325,14 +327,26 @@ __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL]
     if (f == 0x7fffffff) break;
     const uint32_t bm = 1u << bit;
     const int fs = f >> 6, fl = f & 63;
-    const uint32_t plo = __builtin_amdgcn_readlane((int)lo[fs], fl);
-    const uint32_t phi = __builtin_amdgcn_readlane((int)hi[fs], fl);
-    uint32_t pcl = __builtin_amdgcn_readlane((int)cl[fs], fl);
-    uint32_t pch = __builtin_amdgcn_readlane((int)ch[fs], fl);
+    uint32_t plo = 0, phi = 0, pcl = 0, pch = 0;
+    switch (fs) {                                   // uniform: one case runs, no select chains
+#define QLDPC_PIVOT_SLOT(S)                                              \
+  case S:                                                                \
+    if constexpr (S < SF) {                                              \
+      plo = __builtin_amdgcn_readlane((int)lo[S], fl);                   \
+      phi = __builtin_amdgcn_readlane((int)hi[S], fl);                   \
+      pcl = __builtin_amdgcn_readlane((int)cl[S], fl);                   \
+      pch = __builtin_amdgcn_readlane((int)ch[S], fl);                   \
+      fm[S] &= ~(1ull << fl);                       /* no longer free */ \
+    }                                                                    \
+    break;
+      QLDPC_PIVOT_SLOT(0) QLDPC_PIVOT_SLOT(1) QLDPC_PIVOT_SLOT(2) QLDPC_PIVOT_SLOT(3)
+      QLDPC_PIVOT_SLOT(4) QLDPC_PIVOT_SLOT(5) QLDPC_PIVOT_SLOT(6) QLDPC_PIVOT_SLOT(7)
+#undef QLDPC_PIVOT_SLOT
+      default: break;
+    }
     if (K < 32) pcl ^= 1u << K;
     else pch ^= 1u << (K - 32);
     const bool notme = lane != fl;
-    if (!notme) frv &= ~(1u << fs);
 #pragma unroll
     for (int s = 0; s < SF; ++s) {
       if (((HI ? hi[s] : lo[s]) & bm) != 0 && (s != fs || notme)) {   // rows holding a 1,
@@ -365,15 +379,15 @@ __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL]
 // block_half on the smallest power-of-two slot count >= SF (code per count)
 template <int SL, int SFMAX, bool HI>
 __device__ __forceinline__ int block_half_n(int SF, uint32_t (&lo)[SL], uint32_t (&hi)[SL], uint32_t (&cl)[SL],
-                                            uint32_t (&ch)[SL], uint32_t& frv, uint32_t cols, int K,
+                                            uint32_t (&ch)[SL], uint64_t (&fm)[SL], uint32_t cols, int K,
                                             int w, int lane, int& rank, int& nJ, bool& done, uint64_t& pivm,
                                             int rankH, int m, int* pk, int* Jl, unsigned char* inJ) {
   if constexpr (SFMAX > 1) {
     if (SF <= SFMAX / 2)
-      return block_half_n<SL, SFMAX / 2, HI>(SF, lo, hi, cl, ch, frv, cols, K, w, lane, rank, nJ, done, pivm,
+      return block_half_n<SL, SFMAX / 2, HI>(SF, lo, hi, cl, ch, fm, cols, K, w, lane, rank, nJ, done, pivm,
                                              rankH, m, pk, Jl, inJ);
   }
-  return block_half<SL, SFMAX, HI>(lo, hi, cl, ch, frv, cols, K, w, lane, rank, nJ, done, pivm, rankH, m, pk,
+  return block_half<SL, SFMAX, HI>(lo, hi, cl, ch, fm, cols, K, w, lane, rank, nJ, done, pivm, rankH, m, pk,
                                    Jl, inJ);
 }
 
@@ -492,7 +506,7 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
         F += __builtin_popcountll(bf);
       }
       uint32_t lo[SL], hi[SL], cl[SL], ch[SL];
-      uint32_t frv = 0;                               // bit s: compact row 64 s + lane not yet a pivot
+      uint64_t fm[SL];                                // slot s: lanes whose compact row is not yet a pivot
       uint32_t alo = 0, ahi = 0;                      // columns some free row holds
 #pragma unroll
       for (int s = 0; s < SL; ++s) {
@@ -501,7 +515,7 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
         lo[s] = (uint32_t)v;
         hi[s] = (uint32_t)(v >> 32);
         cl[s] = ch[s] = 0;
-        frv |= cp < F ? 1u << s : 0u;
+        fm[s] = __ballot(cp < F);
         alo |= lo[s];
         ahi |= hi[s];
       }
@@ -511,9 +525,9 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
       const int SF = (F + 63) >> 6;
       uint64_t pivm = 0;
       // low half-word columns, then high (each loop's column order ascends)
-      int K = block_half_n<SL, SL, false>(SF, lo, hi, cl, ch, frv, (uint32_t)cols, 0, w, lane, rank, nJ, done,
+      int K = block_half_n<SL, SL, false>(SF, lo, hi, cl, ch, fm, (uint32_t)cols, 0, w, lane, rank, nJ, done,
                                           pivm, a.rank, m, pk, Jl, inJ);
-      K = block_half_n<SL, SL, true>(SF, lo, hi, cl, ch, frv, (uint32_t)(cols >> 32), K, w, lane, rank, nJ, done,
+      K = block_half_n<SL, SL, true>(SF, lo, hi, cl, ch, fm, (uint32_t)(cols >> 32), K, w, lane, rank, nJ, done,
                                      pivm, a.rank, m, pk, Jl, inJ);
 #pragma unroll
       for (int s = 0; s < SL; ++s) {
