@@ -18,6 +18,20 @@ __global__ void k(const double* x, double* t, double* a, double* l, long n) {
   long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
   if (i < n) { t[i] = qldpc_tanh(x[i]); a[i] = qldpc_atanh(x[i]); l[i] = qldpc_log1p(x[i]); }
 }
+__global__ void kd(const double* x, const double* y, double* q, long n) {
+  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (i < n) q[i] = QLDPC_DIV(x[i], y[i]);
+}
+extern "C" int run_div(const double* hx, const double* hy, double* hq, long n) {
+  double *x, *y, *q;
+  if (hipMalloc(&x, n * 8) || hipMalloc(&y, n * 8) || hipMalloc(&q, n * 8)) return 1;
+  hipMemcpy(x, hx, n * 8, hipMemcpyHostToDevice);
+  hipMemcpy(y, hy, n * 8, hipMemcpyHostToDevice);
+  kd<<<(n + 255) / 256, 256>>>(x, y, q, n);
+  hipMemcpy(hq, q, n * 8, hipMemcpyDeviceToHost);
+  hipFree(x); hipFree(y); hipFree(q);
+  return 0;
+}
 extern "C" int run(const double* hx, double* ht, double* ha, double* hl, long n) {
   double *x, *t, *a, *l;
   if (hipMalloc(&x, n * 8) || hipMalloc(&t, n * 8) || hipMalloc(&a, n * 8) || hipMalloc(&l, n * 8)) return 1;
@@ -63,3 +77,34 @@ def test_libm_bit_identical_gpu_vs_host(tmp_path):
     for fn, g, c in zip(("tanh", "atanh", "log1p"), outs["g"], outs["c"]):
         bad = np.flatnonzero(g.view(np.uint64) != c.view(np.uint64))
         assert bad.size == 0, f"{fn}: {bad.size} differ, e.g. x={x[bad[:5]]} gpu={g[bad[:5]]} host={c[bad[:5]]}"
+
+
+def test_device_division_is_ieee_in_range(tmp_path):
+    """QLDPC_DIV on the device (the compiler's division sequence without the
+    v_div_scale / v_div_fixup range steps) equals IEEE a / b bit for bit over
+    the range its callers guarantee: 2^-500 < |a|, |b| < 2^500 or a = 0,
+    including quotients next to 1 (P / t_k), mantissas at the edges of
+    [1, 2) and random exponent pairs."""
+    import qldpcsim_amd._lib  # noqa: F401
+    inc = os.path.join(ROOT, "include")
+    (tmp_path / "g.hip").write_text(HIP_SRC)
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-fPIC", "-shared",
+                    "-I", inc, "-o", str(tmp_path / "g.so"), str(tmp_path / "g.hip")], check=True)
+    rng = np.random.default_rng(7)
+    N = 400000
+    sgn = lambda k: np.where(rng.random(k) < 0.5, -1.0, 1.0)
+    a = np.concatenate([sgn(N) * rng.uniform(1, 2, N) * 2.0 ** rng.integers(-499, 499, N),
+                        sgn(N) * rng.uniform(0, 1, N),
+                        np.nextafter(1.0, 0) ** rng.integers(0, 64, N),
+                        np.zeros(1000), 1 + np.arange(1000) * 2.0 ** -52])
+    b = np.concatenate([sgn(N) * rng.uniform(1, 2, N) * 2.0 ** rng.integers(-499, 499, N),
+                        sgn(N) * (1 - rng.uniform(0, 1, N) * 0.999),
+                        np.nextafter(1.0, 2) ** rng.integers(0, 64, N),
+                        rng.uniform(0.5, 3, 1000), 2 - np.arange(1000) * 2.0 ** -52])
+    q = np.empty_like(a)
+    L = ctypes.CDLL(str(tmp_path / "g.so"))
+    P = lambda v: v.ctypes.data_as(ctypes.c_void_p)
+    assert L.run_div(P(a), P(b), P(q), ctypes.c_long(len(a))) == 0
+    ref = a / b
+    bad = np.flatnonzero(q.view(np.uint64) != ref.view(np.uint64))
+    assert bad.size == 0, f"{bad.size} differ, e.g. a={a[bad[:3]]} b={b[bad[:3]]} gpu={q[bad[:3]]} ieee={ref[bad[:3]]}"
