@@ -84,6 +84,7 @@ struct qldpc_code {
   std::vector<uint32_t> wc, avar;
   uint32_t filt_all = 0;
   uint32_t *d_wc = nullptr, *d_rtab = nullptr;  // rtab: [m][8] relabeled variables per row
+  uint32_t* d_avar = nullptr;                    // [n] filter word per relabeled variable (layered BP)
   // host staging workspace for qldpc_decode_host: device buffers, page-locked
   // host mirrors (DMA copies) and a stream of its own (no device-wide sync)
   std::mutex ws_mu;
@@ -186,6 +187,8 @@ extern "C" int qldpc_code_create(const uint8_t* h_H, int m, int n, qldpc_code** 
       if (e1 == hipSuccess) e1 = hipMemcpy(c->d_wc, c->wc.data(), sizeof(uint32_t) * m, hipMemcpyHostToDevice);
       if (e1 == hipSuccess) e1 = hipMalloc(&c->d_rtab, sizeof(uint32_t) * 8 * m);
       if (e1 == hipSuccess) e1 = hipMemcpy(c->d_rtab, rtab.data(), sizeof(uint32_t) * 8 * m, hipMemcpyHostToDevice);
+      if (e1 == hipSuccess) e1 = hipMalloc(&c->d_avar, sizeof(uint32_t) * n);
+      if (e1 == hipSuccess) e1 = hipMemcpy(c->d_avar, c->avar.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice);
     }
     if (e1 != hipSuccess) {
       delete c;
@@ -220,6 +223,7 @@ extern "C" int qldpc_code_destroy(qldpc_code* code) {
   (void)hipFree(code->d_col_idx);
   (void)hipFree(code->d_wc);
   (void)hipFree(code->d_rtab);
+  (void)hipFree(code->d_avar);
   ws_free(code);
   if (code->ws_stream) (void)hipStreamDestroy(code->ws_stream);
   delete code;
@@ -531,7 +535,7 @@ static void team_layout(const qldpc_code* c, int w, int* bytes, int* off_c2v, in
   *off_parw = off;
   off = align16(off + 4 * words);
   *off_red = off;
-  off = align16(off + 4 * (2 * w + 4));
+  off = align16(off + 4 * (3 * w + 4));   // + [W] filter words (layered stop test)
   *bytes = off;
 }
 
@@ -791,6 +795,7 @@ extern "C" int qldpc_decode_device_ex(const qldpc_code* code, const qldpc_schedu
   a.max_iter = max_iter;
   a.wc = code->d_wc;
   a.rtab = code->d_rtab;
+  a.avar = code->d_avar;
   a.filt_all = code->filt_all;
   {
     // (L + (double)S < 0) == (S < hd_thresh) for every float S: the float at

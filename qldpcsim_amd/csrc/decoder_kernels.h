@@ -42,6 +42,7 @@ struct DecodeArgs {
   const uint32_t* wc;         // [m]   global
   const uint32_t* rtab;       // [m][8] relabeled variables of each row (global; exact stop test)
   uint32_t filt_all;          // XOR of every variable's filter word (all hard decisions 1)
+  const uint32_t* avar;       // [n]   global: filter word per relabeled variable (bp_team_kernel)
   float hd_thresh;            // hard decision of a column sum S: (L + (f64)S < 0) == (S < hd_thresh)
   // bit-packed I/O: syn as uint64 [batch][wm] words, ehat as uint64 [batch][wn]
   // (bit j % 64 of word j / 64) instead of one byte per bit

@@ -1788,10 +1788,8 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
   double* post = (double*)ws;
   double* c2v = (double*)(ws + a.off_c2v);
   uint32_t* synw = (uint32_t*)(ws + a.off_synw);
-  uint32_t* parw = (uint32_t*)(ws + a.off_parw);
   uint32_t* red = (uint32_t*)(ws + a.off_red);          // [2][W] any-slots, [2][2] tickets
   const int m = a.m, n = a.n;
-  const int nwords = (m + 31) >> 5;
   const double L = a.L;
 
   int rphase = 0;
@@ -1831,9 +1829,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
     for (int p = tid; p < a.E; p += TS) c2v[p] = 0.0;
     for (int c0 = 64 * wid; c0 < m; c0 += TS) {
       const int c = c0 + lane;
-      const int in = c < m;
-      store_bits64(synw, c0, in ? (int)syn_bit(a, hs, c) : 0, lane);
-      if constexpr (LAYERED) store_bits64(parw, c0, in && (L < 0.0) && (DC & 1), lane);
+      store_bits64(synw, c0, c < m ? (int)syn_bit(a, hs, c) : 0, lane);
     }
     __syncthreads();
 
@@ -1868,6 +1864,18 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
         }
       }
     } else {
+      // Stop test after every layer (:283-285) by ms_layered_kernel's 32
+      // parity filters: B = the syndrome's filter parities, F
+      // = the hard decisions', kept current with the filter word of every
+      // variable the VN flips; only F == B (convergence, or a 2^-32 false
+      // match) runs the exact row check. Each wave posts its flips' XOR in a
+      // slot read after the VN barrier, so a layer costs two team barriers,
+      // not three, and no parity atomics.
+      uint32_t bl = 0;
+      for (int c = lane; c < m; c += 64) bl ^= ((synw[c >> 5] >> (c & 31)) & 1u) ? a.wc[c] : 0u;
+      const uint32_t B = wave_xor(bl);
+      uint32_t F = (L < 0.0) ? a.filt_all : 0u;           // every post starts at L
+      uint32_t* fsl = red + 2 * W + 4;                    // [W] filter words of this layer's flips
       for (int it = 0; it < a.max_iter && !conv; ++it) {
         for (int l = 0; l < a.n_layers; ++l) {
           const int q0 = g.lay_ptr[l], q1 = g.lay_ptr[l + 1];
@@ -1879,28 +1887,34 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
             (void)cn_bp_group<DC>(a, g, c, valid, k, lane, sb, post, c2v, fl);
           }
           __syncthreads();
-          // VN over the layer's adjacent variables; flips toggle check parities
+          // VN over the layer's adjacent variables
           const int v0 = g.adj_ptr[l], v1 = g.adj_ptr[l + 1];
+          uint32_t acc = 0;
           for (int q = v0 + tid; q < v1; q += TS) {
             const int j = g.adj_vars[q];
             const double old = post[j];
             const double nw = vn_post<ALGO_BP>(a, g, j, c2v, -1);
             post[j] = nw;
-            if ((old < 0.0) != (nw < 0.0)) {
-              const uint32_t info = g.vn_info[j];
-              for (int p = (int)(info & 0xffffu), pe = p + (int)(info >> 16); p < pe; ++p) {
-                const int c = g.vn_chk[p];
-                atomicXor(&parw[c >> 5], 1u << (c & 31));
-              }
-            }
+            if ((old < 0.0) != (nw < 0.0)) acc ^= a.avar[j];   // hard decision flipped
           }
+          const uint32_t wacc = wave_xor(acc);
+          if (lane == 0) fsl[wid] = wacc;
           __syncthreads();
-          uint32_t un = 0;                               // stop test after every layer (:283-285)
-          for (int w = tid; w < nwords; w += TS) un |= parw[w] ^ synw[w];
-          if (!team_any(un != 0)) {
-            iters = it + 1;
-            conv = true;
-            break;
+#pragma unroll
+          for (int w = 0; w < W; ++w) F ^= fsl[w];
+          if (F == B) {                                   // team-uniform
+            uint32_t un = 0;
+            for (int c = tid; c < m; c += TS) {
+              uint32_t par = 0;
+#pragma unroll
+              for (int q = 0; q < DC; ++q) par ^= (uint32_t)(post[tab_var<DC>(g.cn_tab[8 * c + q])] < 0.0);
+              un |= par ^ ((synw[c >> 5] >> (c & 31)) & 1u);
+            }
+            if (!team_any(un != 0)) {
+              iters = it + 1;
+              conv = true;
+              break;
+            }
           }
         }
       }
