@@ -1842,13 +1842,17 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
           const uint32_t sb = valid ? (synw[c >> 5] >> (c & 31)) & 1u : 0u;
           unsat |= cn_bp_group<DC>(a, g, valid ? c : 0, valid, k, lane, sb, post, c2v, fl);
         }
-        // the parity pass is the stop test of iteration it-1 (:283-285)
-        if (it > 0 && !team_any(unsat != 0)) {
-          iters = it;
-          conv = true;
-          break;
+        // the parity pass is the stop test of iteration it-1 (:283-285); its
+        // team barrier also orders these c2v writes before the VN reads them
+        if (it > 0) {
+          if (!team_any(unsat != 0)) {
+            iters = it;
+            conv = true;
+            break;
+          }
+        } else {
+          __syncthreads();
         }
-        __syncthreads();
         for (int j = tid; j < n; j += TS) post[j] = vn_post<ALGO_BP>(a, g, j, c2v, -1);
         __syncthreads();
         if (it + 1 == a.max_iter) {
