@@ -1713,7 +1713,8 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_grp_kernel(Decod
 // lanes on one half-shot's state: more waves per CU for the same LDS, and a
 // layered layer (30-60 checks) becomes one pass of 8-lane groups.
 // Variable nodes: one lane per variable (np.sum pairwise rule), as before.
-// Team-wide stop tests go through LDS slots (double-buffered, one barrier).
+// Team-wide stop tests go through LDS slots (double-buffered, one barrier);
+// layered: parity filters posted per wave (see the layered branch).
 // ---------------------------------------------------------------------------
 template <int DC>
 __device__ __forceinline__ uint32_t cn_bp_group(const DecodeArgs& a, const LdsView& g, int c, bool valid,
