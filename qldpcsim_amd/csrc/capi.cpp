@@ -246,6 +246,7 @@ struct LaunchCfg {
   int waves = 0, blocks_per_cu = 0, lds = 0, wave_bytes = 0;
   bool lblob = false;  // uses the layer-ordered blob (ms_layered_kernel)
   bool gtab = false;     // ms_flood_kernel: global tables, LDS = wave state only
+  bool tgt = false;      // bp_team_kernel<.., true>: row table global, LDS image = tblob
   int team = 0;          // bp_team_kernel: waves per half-shot (one workgroup), 0 = wave kernels
   int nh = 1;            // ms_layered_grp_kernel: half-shots per wave
   int slice = 0;         // ms_layered_grp_kernel: bytes of one half-shot's LDS slice
@@ -268,6 +269,12 @@ struct qldpc_schedule {
   int off_cn_tab = 0, off_row_ptr = 0, off_vn_ptr = 0, off_vn_chk = 0;
   int off_lay_ptr = 0, off_lay_rows = 0, off_adj_ptr = 0, off_adj_vars = 0, off_chunk_dmax = 0;
   unsigned char* d_blob = nullptr;
+  // layered BP teams (bp_team_kernel<true, DC, W, true>): variable and layer
+  // tables first (the LDS image), then the row table read from global memory
+  std::vector<uint8_t> tblob;
+  unsigned char* d_tblob = nullptr;
+  int t_lds_bytes = 0, t_off_cn_tab = 0, t_off_vn_ptr = 0, t_off_lay_ptr = 0, t_off_lay_rows = 0,
+      t_off_adj_ptr = 0, t_off_adj_vars = 0;
   // flooding MS, uniform degree: global table image of ms_flood_kernel
   std::vector<uint8_t> fblob;
   unsigned char* d_fblob = nullptr;
@@ -386,6 +393,17 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
       std::sort(rows.begin(), rows.end());
       s->median_rows = n_layers ? rows[n_layers / 2] : 0;
     }
+    if (fast_table_ok(code)) {
+      s->t_off_vn_ptr = put(s->tblob, vn_ptr);
+      s->t_off_lay_ptr = put(s->tblob, lay_ptr);
+      s->t_off_lay_rows = put(s->tblob, lay_rows);
+      s->t_off_adj_ptr = put(s->tblob, adj_ptr);
+      s->t_off_adj_vars = put(s->tblob, adj_vars);
+      s->tblob.resize(align16((int)s->tblob.size() + 1));
+      s->t_lds_bytes = (int)s->tblob.size();
+      s->t_off_cn_tab = put(s->tblob, cn_tab);
+      s->tblob.resize(align16((int)s->tblob.size() + 1));
+    }
     s->off_vn_chk = put(s->blob, vn_chk);
     s->off_lay_ptr = put(s->blob, lay_ptr);
     s->off_lay_rows = put(s->blob, lay_rows);
@@ -476,6 +494,10 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
     e1 = hipMalloc(&s->d_fblob, s->fblob.size());
     if (e1 == hipSuccess) e1 = hipMemcpy(s->d_fblob, s->fblob.data(), s->fblob.size(), hipMemcpyHostToDevice);
   }
+  if (e1 == hipSuccess && !s->tblob.empty()) {
+    e1 = hipMalloc(&s->d_tblob, s->tblob.size());
+    if (e1 == hipSuccess) e1 = hipMemcpy(s->d_tblob, s->tblob.data(), s->tblob.size(), hipMemcpyHostToDevice);
+  }
   if (e1 == hipSuccess && !s->lblob.empty()) {
     e1 = hipMalloc(&s->d_lblob, s->lblob.size());
     if (e1 == hipSuccess) e1 = hipMemcpy(s->d_lblob, s->lblob.data(), s->lblob.size(), hipMemcpyHostToDevice);
@@ -492,6 +514,7 @@ extern "C" int qldpc_schedule_destroy(qldpc_schedule* s) {
   if (!s) return QLDPC_OK;
   (void)hipFree(s->d_blob);
   (void)hipFree(s->d_lblob);
+  (void)hipFree(s->d_tblob);
   (void)hipFree(s->d_fblob);
   (void)hipFree(s->d_queue);
   delete s;
@@ -588,8 +611,26 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
     int tb = 0, o1, o2, o3, o4;
     team_layout(c, 4, &tb, &o1, &o2, &o3, &o4);
     team = ((int)s->blob.size() + tb > 48 * 1024) ? 8 : 4;
+    // Layered: 4-wave teams with the row table in global memory when the
+    // compact LDS image fits more teams per CU (LP118_2: 3 instead of 2; the
+    // kernel is latency-bound, and BP-L p = 0.1 ran 175 -> 132 ms per launch).
+    // A CU holds at most 16 team waves (VGPR cap of 4 waves per SIMD).
+    bool tgt = false;
+    if (s->layered && !s->tblob.empty()) {
+      int dev0 = 0, lds_max = 0, tb8 = 0;
+      if (hipGetDevice(&dev0) == hipSuccess &&
+          hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev0) == hipSuccess) {
+        team_layout(c, team, &tb8, &o1, &o2, &o3, &o4);
+        const int std_teams = std::min(lds_max / ((int)s->blob.size() + tb8), 16 / team);
+        const int gt_teams = std::min(lds_max / (s->t_lds_bytes + tb), 16 / 4);
+        tgt = gt_teams > std_teams;
+      }
+    }
+    if (const char* ev = getenv("QLDPC_BP_GT")) tgt = s->layered && !s->tblob.empty() && atoi(ev) != 0;
+    if (tgt) team = 4;
     if (const char* ev = getenv("QLDPC_BP_TEAM_W")) team = atoi(ev);
-    cfg.kernel = qldpc::select_bp_team_kernel(s->layered, dc, team, &cfg.name);
+    cfg.kernel = qldpc::select_bp_team_kernel(s->layered, dc, team, tgt, &cfg.name);
+    cfg.tgt = tgt && cfg.kernel != nullptr;
     if (!cfg.kernel) team = 0;
   }
   cfg.team = team;
@@ -605,7 +646,9 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   HIP_TRY(hipGetDevice(&dev));
   HIP_TRY(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
   HIP_TRY(qldpc::configure_kernel(cfg.kernel, max_lds));
-  const int blob = gtab ? QLDPC_FLOOD_HDR : (int)(use_lblob ? s->lblob.size() : s->blob.size());
+  const int blob = gtab ? QLDPC_FLOOD_HDR
+                        : cfg.tgt ? s->t_lds_bytes
+                        : (int)(use_lblob ? s->lblob.size() : s->blob.size());
   int best_waves = 0;
   if (team) {  // one team (workgroup of `team` waves) per half-shot
     const int lds = blob + cfg.wave_bytes;
@@ -766,6 +809,17 @@ extern "C" int qldpc_decode_device_ex(const qldpc_code* code, const qldpc_schedu
     a.off_vn_chk = sched->l_off_vn_chk;
   }
   if (cfg->team) team_layout(code, cfg->team, &a.wave_bytes, &a.off_c2v, &a.off_synw, &a.off_parw, &a.off_red);
+  if (cfg->tgt) {  // bp_team_kernel<.., true>: LDS part of tblob + its global row table
+    a.blob = sched->d_tblob;
+    a.blob_bytes = sched->t_lds_bytes;
+    a.off_cn_tab = sched->t_off_cn_tab;
+    a.off_vn_ptr = sched->t_off_vn_ptr;
+    a.off_lay_ptr = sched->t_off_lay_ptr;
+    a.off_lay_rows = sched->t_off_lay_rows;
+    a.off_adj_ptr = sched->t_off_adj_ptr;
+    a.off_adj_vars = sched->t_off_adj_vars;
+    a.off_row_ptr = a.off_chunk_dmax = a.off_vn_chk = 0;   // (not read by the team kernel)
+  }
   if (cfg->slice) grp_layout(code, &a.wave_bytes, &a.off_c2v, &a.off_synw);   // per half-shot slice
   if (cfg->gtab) {  // global tables; the LDS holds wave state only
     a.blob = sched->d_fblob;

@@ -60,7 +60,8 @@ const void* select_ms_layered_kernel(int dc, int g, const char** name);
 // layered MS, NH half-shots per wave (64 / NH lanes each), G lanes per check
 const void* select_ms_layered_grp_kernel(int dc, int nh, int g, const char** name);
 // BP, uniform row degree 7/8: one team of W waves per half-shot, edge-parallel check nodes
-const void* select_bp_team_kernel(bool layered, int dc, int w, const char** name);
+// gt: the row table in global memory, LDS image = the team blob (tblob)
+const void* select_bp_team_kernel(bool layered, int dc, int w, bool gt, const char** name);
 hipError_t launch_decode(const void* kernel, const DecodeArgs& args, int grid, int block,
                          int lds_bytes, hipStream_t stream);
 hipError_t configure_kernel(const void* kernel, int lds_bytes);

@@ -1759,7 +1759,11 @@ __device__ __forceinline__ uint32_t cn_bp_group(const DecodeArgs& a, const LdsVi
   return valid ? (par ^ synb) : 0u;
 }
 
-template <bool LAYERED, int DC, int W>
+// GT: the check-row table (8 words per check) is read from global memory
+// (L1/L2-resident) and the LDS image holds only the variable / layer tables
+// (tblob, capi.cpp): LP118_2's 34 KB image shrinks to 12 KB, so a CU holds 3
+// teams' float64 state instead of 2.
+template <bool LAYERED, int DC, int W, bool GT = false>
 __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) bp_team_kernel(DecodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   {
@@ -1770,7 +1774,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
   }
   __syncthreads();
   LdsView g;
-  g.cn_tab = (const uint32_t*)(lds + a.off_cn_tab);
+  g.cn_tab = GT ? (const uint32_t*)(a.blob + a.off_cn_tab) : (const uint32_t*)(lds + a.off_cn_tab);
   g.row_ptr = (const uint16_t*)(lds + a.off_row_ptr);
   g.vn_info = (const uint32_t*)(lds + a.off_vn_ptr);
   g.chunk_dmax = (const uint8_t*)(lds + a.off_chunk_dmax);
@@ -1976,12 +1980,17 @@ const void* select_ms_flood_kernel(int dc, int kc, const char** name) {
   return nullptr;
 }
 
-const void* select_bp_team_kernel(bool layered, int dc, int w, const char** name) {
+const void* select_bp_team_kernel(bool layered, int dc, int w, bool gt, const char** name) {
 #define QLDPC_BPT(L, D, Wn) \
-  if (layered == L && dc == D && w == Wn) QLDPC_NAMED((&bp_team_kernel<L, D, Wn>), "bp_team_kernel<" #L ", " #D ", " #Wn ">");
+  if (!gt && layered == L && dc == D && w == Wn) QLDPC_NAMED((&bp_team_kernel<L, D, Wn>), "bp_team_kernel<" #L ", " #D ", " #Wn ">");
   QLDPC_BPT(false, 7, 4) QLDPC_BPT(false, 8, 4) QLDPC_BPT(true, 7, 4) QLDPC_BPT(true, 8, 4)
   QLDPC_BPT(false, 7, 8) QLDPC_BPT(false, 8, 8) QLDPC_BPT(true, 7, 8) QLDPC_BPT(true, 8, 8)
 #undef QLDPC_BPT
+#define QLDPC_BPG(L, D, Wn)                                  \
+  if (gt && layered == L && dc == D && w == Wn)              \
+    QLDPC_NAMED((&bp_team_kernel<L, D, Wn, true>), "bp_team_kernel<" #L ", " #D ", " #Wn ", true>");
+  QLDPC_BPG(true, 7, 4) QLDPC_BPG(true, 8, 4) QLDPC_BPG(true, 7, 8) QLDPC_BPG(true, 8, 8)
+#undef QLDPC_BPG
   return nullptr;
 }
 

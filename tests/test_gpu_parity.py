@@ -130,7 +130,7 @@ def _channel(Hx, Hz, p, B, seed):
     ("LP118_0", "F", "BP", None, 5, 512),         # short horizon: every posterior within tolerance
     ("LP118_0", "L", "BP", None, 3, 256),
     ("LP118_0", "L", "MS", 0.05, 50, 2048),
-    ("LP118_2", "L", "BP", 0.08, 100, 128),       # BP team kernel, 8 waves per half-shot
+    ("LP118_2", "L", "BP", 0.08, 100, 128),       # BP team kernel, 4-wave teams, global row table
     ("LP118_2", "F", "BP", None, 4, 128),
     ("LP04_0", "F", "BP", 0.1, 100, 512),         # BP team kernel, row degree 7
     ("LP118_0", "S", "MS", 0.05, 3, 256),
@@ -326,6 +326,37 @@ def test_ms_layered_irregular_columns_match_oracle(dec, sched):
                           .astype(np.uint8)])
     r = dec.decode_batch(H, syn, 0.05 / 3, 25, algo="MS", want_post=True, layer_ptr=lp, layer_rows=lr)
     e, it, post, fl = oracle.decode_batch("MS", H, syn, 0.05 / 3, 25, lp, lr)
+    np.testing.assert_array_equal(r.iters, it)
+    np.testing.assert_array_equal(r.ehat, e)
+    np.testing.assert_array_equal(r.post.view(np.uint64), post.view(np.uint64))
+
+
+@pytest.mark.parametrize("code,w,gt", [("LP118_2", "4", "1"), ("LP118_2", "8", "1"), ("LP04_0", "4", "1"),
+                                        ("LP118_0", "8", "1"), ("LP118_2", "8", "0"), ("LP118_2", "4", "0")])
+def test_bp_team_global_row_table_matches_oracle(dec, code, w, gt, monkeypatch):
+    """Layered BP teams with the row table in global memory and the compact
+    LDS image (bp_team_kernel<true, DC, W, true>, QLDPC_BP_GT=1; LP118_2's
+    default) at both team widths, and the all-LDS team kernel (gt 0):
+    bit-exact vs the oracle on channel and fixed-work syndromes."""
+    from oracle import oracle
+    from qldpcsim_amd import _lib, codes, schedule
+    monkeypatch.setenv("QLDPC_BP_GT", gt)
+    monkeypatch.setenv("QLDPC_BP_TEAM_W", w)
+    Hx, Hz = codes.load_code(code)
+    lx, _ = schedule.select_layers(Hx, Hz, "L")
+    lp, lr = schedule.pack_layers(lx, Hz.shape[0])
+    rng = np.random.default_rng(17)
+    syn = np.concatenate([rng.integers(0, 2, (32, Hz.shape[0]), dtype=np.uint8),
+                          _channel(Hx, Hz, 0.08, 160, 9)[0]])
+    code_h = _lib.code_for(Hz)
+    code_h._sched.clear()                  # launch configs read the env once per schedule
+    try:
+        nm = _lib.kernel_name(Hz, lp, lr, "BP")
+        assert nm.startswith("bp_team_kernel<true") and nm.endswith(f", {w}, true>" if gt == "1" else f", {w}>"), nm
+        r = dec.decode_batch(Hz, syn, 0.08 / 3, 40, algo="BP", want_post=True, layer_ptr=lp, layer_rows=lr)
+    finally:
+        code_h._sched.clear()
+    e, it, post, _ = oracle.decode_batch("BP", Hz, syn, 0.08 / 3, 40, lp, lr)
     np.testing.assert_array_equal(r.iters, it)
     np.testing.assert_array_equal(r.ehat, e)
     np.testing.assert_array_equal(r.post.view(np.uint64), post.view(np.uint64))
