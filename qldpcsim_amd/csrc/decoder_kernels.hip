@@ -1982,7 +1982,7 @@ const void* select_ms_flood_kernel(int dc, int kc, const char** name) {
 
 const void* select_bp_team_kernel(bool layered, int dc, int w, bool gt, const char** name) {
 #define QLDPC_BPT(L, D, Wn) \
-  if (!gt && layered == L && dc == D && w == Wn) QLDPC_NAMED((&bp_team_kernel<L, D, Wn>), "bp_team_kernel<" #L ", " #D ", " #Wn ">");
+  if (!gt && layered == L && dc == D && w == Wn) QLDPC_NAMED((&bp_team_kernel<L, D, Wn>), "bp_team_kernel<" #L ", " #D ", " #Wn ", false>");
   QLDPC_BPT(false, 7, 4) QLDPC_BPT(false, 8, 4) QLDPC_BPT(true, 7, 4) QLDPC_BPT(true, 8, 4)
   QLDPC_BPT(false, 7, 8) QLDPC_BPT(false, 8, 8) QLDPC_BPT(true, 7, 8) QLDPC_BPT(true, 8, 8)
 #undef QLDPC_BPT
