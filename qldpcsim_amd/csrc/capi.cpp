@@ -247,6 +247,7 @@ struct LaunchCfg {
   bool lblob = false;  // uses the layer-ordered blob (ms_layered_kernel)
   bool gtab = false;     // ms_flood_kernel: global tables, LDS = wave state only
   bool tgt = false;      // bp_team_kernel<.., true>: row table global, LDS image = tblob
+  bool tlg = false;      // bp_team_lg_kernel: every table global, LDS image = layer pointers
   int team = 0;          // bp_team_kernel: waves per half-shot (one workgroup), 0 = wave kernels
   int nh = 1;            // ms_layered_grp_kernel: half-shots per wave
   int slice = 0;         // ms_layered_grp_kernel: bytes of one half-shot's LDS slice
@@ -273,6 +274,11 @@ struct qldpc_schedule {
   // tables first (the LDS image), then the row table read from global memory
   std::vector<uint8_t> tblob;
   unsigned char* d_tblob = nullptr;
+  // layered BP teams with every table global (bp_team_lg_kernel): layer
+  // pointers (the LDS image), then rows in layer order, their checks, adjacency
+  std::vector<uint8_t> lgblob;
+  unsigned char* d_lgblob = nullptr;
+  int lg_lds_bytes = 0, lg_off_lay_ptr = 0, lg_off_adj_ptr = 0, lg_off_ltab = 0, lg_off_lrow = 0, lg_off_adj = 0;
   int t_lds_bytes = 0, t_off_cn_tab = 0, t_off_vn_ptr = 0, t_off_lay_ptr = 0, t_off_lay_rows = 0,
       t_off_adj_ptr = 0, t_off_adj_vars = 0;
   // flooding MS, uniform degree: global table image of ms_flood_kernel
@@ -435,6 +441,19 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
         adj_dmax[l] = (uint8_t)(adj_dmax[l] | (gl << 5));
         s->layer_g = (s->layer_g == -2 || s->layer_g == (1 << gl)) ? (1 << gl) : 0;
       }
+      {
+        std::vector<uint32_t> btab((size_t)8 * lay_rows.size(), 0);   // cn_tab words (BP format), layer order
+        for (size_t q = 0; q < lay_rows.size(); ++q)
+          for (int k = 0; k < 8; ++k) btab[8 * q + k] = cn_tab[(size_t)8 * lay_rows[q] + k];
+        s->lg_off_lay_ptr = put(s->lgblob, lay_ptr);
+        s->lg_off_adj_ptr = put(s->lgblob, adj_ptr);
+        s->lgblob.resize(align16((int)s->lgblob.size() + 1));
+        s->lg_lds_bytes = (int)s->lgblob.size();
+        s->lg_off_ltab = put(s->lgblob, btab);
+        s->lg_off_lrow = put(s->lgblob, lay_rows);
+        s->lg_off_adj = put(s->lgblob, adj_info);
+        s->lgblob.resize(align16((int)s->lgblob.size() + 1));
+      }
       s->l_off_ltab = put(s->lblob, ltab);
       s->l_off_lrow = put(s->lblob, lay_rows);
       s->l_off_lay_ptr = put(s->lblob, lay_ptr);
@@ -494,6 +513,10 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
     e1 = hipMalloc(&s->d_fblob, s->fblob.size());
     if (e1 == hipSuccess) e1 = hipMemcpy(s->d_fblob, s->fblob.data(), s->fblob.size(), hipMemcpyHostToDevice);
   }
+  if (e1 == hipSuccess && !s->lgblob.empty()) {
+    e1 = hipMalloc(&s->d_lgblob, s->lgblob.size());
+    if (e1 == hipSuccess) e1 = hipMemcpy(s->d_lgblob, s->lgblob.data(), s->lgblob.size(), hipMemcpyHostToDevice);
+  }
   if (e1 == hipSuccess && !s->tblob.empty()) {
     e1 = hipMalloc(&s->d_tblob, s->tblob.size());
     if (e1 == hipSuccess) e1 = hipMemcpy(s->d_tblob, s->tblob.data(), s->tblob.size(), hipMemcpyHostToDevice);
@@ -515,6 +538,7 @@ extern "C" int qldpc_schedule_destroy(qldpc_schedule* s) {
   (void)hipFree(s->d_blob);
   (void)hipFree(s->d_lblob);
   (void)hipFree(s->d_tblob);
+  (void)hipFree(s->d_lgblob);
   (void)hipFree(s->d_fblob);
   (void)hipFree(s->d_queue);
   delete s;
@@ -611,26 +635,26 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
     int tb = 0, o1, o2, o3, o4;
     team_layout(c, 4, &tb, &o1, &o2, &o3, &o4);
     team = ((int)s->blob.size() + tb > 48 * 1024) ? 8 : 4;
-    // Layered: 4-wave teams with the row table in global memory when the
-    // compact LDS image fits more teams per CU (LP118_2: 3 instead of 2; the
-    // kernel is latency-bound, and BP-L p = 0.1 ran 175 -> 132 ms per launch).
-    // A CU holds at most 16 team waves (VGPR cap of 4 waves per SIMD).
+    // Layered: 4-wave teams with every graph table in global memory
+    // (bp_team_lg_kernel): LDS holds only the team's state, so a CU runs 4
+    // teams (the VGPR cap of 16 team waves) — LP118_2: 2 teams with all-LDS
+    // tables, 3 with the row table alone global; the kernel is barrier /
+    // latency-bound and BP-L p = 0.1 ran 175 -> 132 -> 108 ms per launch.
+    // QLDPC_BP_GT=0 (all LDS) / 1 (row table global) / 2 (default) override.
     bool tgt = false;
-    if (s->layered && !s->tblob.empty()) {
-      int dev0 = 0, lds_max = 0, tb8 = 0;
-      if (hipGetDevice(&dev0) == hipSuccess &&
-          hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev0) == hipSuccess) {
-        team_layout(c, team, &tb8, &o1, &o2, &o3, &o4);
-        const int std_teams = std::min(lds_max / ((int)s->blob.size() + tb8), 16 / team);
-        const int gt_teams = std::min(lds_max / (s->t_lds_bytes + tb), 16 / 4);
-        tgt = gt_teams > std_teams;
-      }
+    bool tlg = s->layered && !s->lgblob.empty();
+    if (const char* ev = getenv("QLDPC_BP_GT")) {
+      tgt = s->layered && !s->tblob.empty() && atoi(ev) == 1;
+      tlg = s->layered && !s->lgblob.empty() && atoi(ev) == 2;
     }
-    if (const char* ev = getenv("QLDPC_BP_GT")) tgt = s->layered && !s->tblob.empty() && atoi(ev) != 0;
-    if (tgt) team = 4;
+    if (tgt || tlg) team = 4;
     if (const char* ev = getenv("QLDPC_BP_TEAM_W")) team = atoi(ev);
-    cfg.kernel = qldpc::select_bp_team_kernel(s->layered, dc, team, tgt, &cfg.name);
-    cfg.tgt = tgt && cfg.kernel != nullptr;
+    if (tlg) {
+      cfg.kernel = qldpc::select_bp_team_lg_kernel(dc, team, &cfg.name);
+      cfg.tlg = cfg.kernel != nullptr;
+    }
+    if (!cfg.kernel) cfg.kernel = qldpc::select_bp_team_kernel(s->layered, dc, team, tgt, &cfg.name);
+    cfg.tgt = tgt && !cfg.tlg && cfg.kernel != nullptr;
     if (!cfg.kernel) team = 0;
   }
   cfg.team = team;
@@ -648,6 +672,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   HIP_TRY(qldpc::configure_kernel(cfg.kernel, max_lds));
   const int blob = gtab ? QLDPC_FLOOD_HDR
                         : cfg.tgt ? s->t_lds_bytes
+                        : cfg.tlg ? s->lg_lds_bytes
                         : (int)(use_lblob ? s->lblob.size() : s->blob.size());
   int best_waves = 0;
   if (team) {  // one team (workgroup of `team` waves) per half-shot
@@ -809,6 +834,15 @@ extern "C" int qldpc_decode_device_ex(const qldpc_code* code, const qldpc_schedu
     a.off_vn_chk = sched->l_off_vn_chk;
   }
   if (cfg->team) team_layout(code, cfg->team, &a.wave_bytes, &a.off_c2v, &a.off_synw, &a.off_parw, &a.off_red);
+  if (cfg->tlg) {  // bp_team_lg_kernel: layer pointers in LDS, every table global
+    a.blob = sched->d_lgblob;
+    a.blob_bytes = sched->lg_lds_bytes;
+    a.off_lay_ptr = sched->lg_off_lay_ptr;
+    a.off_adj_ptr = sched->lg_off_adj_ptr;
+    a.off_cn_tab = sched->lg_off_ltab;
+    a.off_lay_rows = sched->lg_off_lrow;
+    a.off_row_ptr = sched->lg_off_adj;
+  }
   if (cfg->tgt) {  // bp_team_kernel<.., true>: LDS part of tblob + its global row table
     a.blob = sched->d_tblob;
     a.blob_bytes = sched->t_lds_bytes;

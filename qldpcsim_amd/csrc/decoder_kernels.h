@@ -57,6 +57,8 @@ const void* select_ms_flood_kernel(int dc, int kc, const char** name);  // nullp
 int ms_flood_max_waves(int kc);                      // waves per workgroup it was compiled for
 // layered MS, uniform row degree 7/8, G = 1/2/4/8 lanes per check (layer-table blob)
 const void* select_ms_layered_kernel(int dc, int g, const char** name);
+// layered BP teams, every graph table in global memory (gblob of the schedule)
+const void* select_bp_team_lg_kernel(int dc, int w, const char** name);
 // layered MS, NH half-shots per wave (64 / NH lanes each), G lanes per check
 const void* select_ms_layered_grp_kernel(int dc, int nh, int g, const char** name);
 // BP, uniform row degree 7/8: one team of W waves per half-shot, edge-parallel check nodes

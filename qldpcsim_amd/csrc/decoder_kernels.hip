@@ -1716,12 +1716,11 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_grp_kernel(Decod
 // Team-wide stop tests go through LDS slots (double-buffered, one barrier);
 // layered: parity filters posted per wave (see the layered branch).
 // ---------------------------------------------------------------------------
+// edge k of a check whose table word t (row table entry 8c + k) is given
 template <int DC>
-__device__ __forceinline__ uint32_t cn_bp_group(const DecodeArgs& a, const LdsView& g, int c, bool valid,
-                                                int k, int lane, uint32_t synb, const double* post,
-                                                double* c2v, int& fl) {
+__device__ __forceinline__ uint32_t cn_bp_word(const DecodeArgs& a, uint32_t t, bool valid, int k, int lane,
+                                               uint32_t synb, const double* post, double* c2v, int& fl) {
   const bool ek = valid && k < DC;
-  const uint32_t t = ek ? g.cn_tab[8 * c + k] : 0u;
   const int j = (int)((t & 0xffffu) >> 3), p = (int)(t >> 18);
   const double pj = ek ? post[j] : 0.0;
   double th = 1.0;
@@ -1757,6 +1756,14 @@ __device__ __forceinline__ uint32_t cn_bp_group(const DecodeArgs& a, const LdsVi
     c2v[p] = val;
   }
   return valid ? (par ^ synb) : 0u;
+}
+
+template <int DC>
+__device__ __forceinline__ uint32_t cn_bp_group(const DecodeArgs& a, const LdsView& g, int c, bool valid,
+                                                int k, int lane, uint32_t synb, const double* post,
+                                                double* c2v, int& fl) {
+  const uint32_t t = (valid && k < DC) ? g.cn_tab[8 * c + k] : 0u;
+  return cn_bp_word<DC>(a, t, valid, k, lane, synb, post, c2v, fl);
 }
 
 // GT: the check-row table (8 words per check) is read from global memory
@@ -1957,6 +1964,195 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
 }
 
 // ---------------------------------------------------------------------------
+// Layered BP teams with every graph table in global memory (L1/L2-resident):
+// the rows in layer order (8 table words each) and their check indices, and
+// per adjacency slot of a layer its (variable, degree, CSC start) word. LDS
+// then holds only the team's float64 state (LP118_2: 37 KB), so a CU holds
+// 4 four-wave teams (the VGPR cap) instead of 3 with the row table alone in
+// global memory or 2 with every table in LDS. The table reads are issued a
+// phase ahead: this layer's adjacency words while its check nodes run, the
+// next layer's row words while this layer's variable nodes run. Same
+// arithmetic as bp_team_kernel<true, DC, W>, bit for bit.
+// ---------------------------------------------------------------------------
+template <int DC, int W>
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) bp_team_lg_kernel(DecodeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  {
+    const uint4* src = (const uint4*)a.blob;                    // LDS part: layer pointers
+    uint4* dst = (uint4*)lds;
+    const int nvec = a.blob_bytes >> 4;
+    for (int i = threadIdx.x; i < nvec; i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  const uint32_t* ltab_g = (const uint32_t*)(a.blob + a.off_cn_tab);      // [Q][8] rows, layer order
+  const uint16_t* lrow_g = (const uint16_t*)(a.blob + a.off_lay_rows);    // [Q]    their checks
+  const uint32_t* adj_g = (const uint32_t*)(a.blob + a.off_row_ptr);      // [A]    var<<21 | deg<<16 | start
+  const uint16_t* lay_ptr = (const uint16_t*)(lds + a.off_lay_ptr);
+  const uint16_t* adj_ptr = (const uint16_t*)(lds + a.off_adj_ptr);
+
+  constexpr int TS = 64 * W;        // threads per team
+  constexpr int GP = 8 * W;         // 8-lane check groups per pass
+  constexpr int NPF = 2;            // CN passes prefetched per layer
+  constexpr int NAF = 2;            // VN slots prefetched per thread
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int grp = tid >> 3, k = tid & 7;
+  unsigned char* ws = lds + a.blob_bytes;
+  double* post = (double*)ws;
+  double* c2v = (double*)(ws + a.off_c2v);
+  uint32_t* synw = (uint32_t*)(ws + a.off_synw);
+  uint32_t* red = (uint32_t*)(ws + a.off_red);
+  const int m = a.m, n = a.n, nl = a.n_layers;
+  const double L = a.L;
+
+  int rphase = 0;
+  auto team_any = [&](bool pred) -> bool {              // one barrier
+    const uint64_t b = ballot(pred);
+    if (lane == 0) red[rphase * W + wid] = b != 0;
+    __syncthreads();
+    bool r = false;
+#pragma unroll
+    for (int w = 0; w < W; ++w) r |= red[rphase * W + w] != 0;
+    rphase ^= 1;
+    return r;
+  };
+  uint32_t pt[NPF], pc[NPF];                            // prefetched row words / checks
+  auto rows_pf = [&](int l) {
+    const int q0 = lay_ptr[l], q1 = lay_ptr[l + 1];
+#pragma unroll
+    for (int i = 0; i < NPF; ++i) {
+      const int q = q0 + GP * i + grp;
+      const bool v = q < q1;
+      pt[i] = (v && k < DC) ? ltab_g[8 * q + k] : 0u;
+      pc[i] = v ? lrow_g[q] : 0u;
+    }
+  };
+
+  long long hs = blockIdx.x, end = hs + 1;
+  const long long stride = gridDim.x;
+  uint32_t seen = 0, tlen = 1, tk = 0;
+  int tphase = 0;
+  while (hs < a.batch) {
+    bool claimed = false;
+    if (a.queue && hs + 1 == end) {
+      const long long rem = a.batch - stride - (long long)seen;
+      long long len = rem / (4 * stride);
+      len = len < 1 ? 1 : (len > 64 ? 64 : len);
+      tlen = (uint32_t)len;
+      claimed = true;
+      if (tid == 0) tk = atomicAdd(a.queue, tlen);
+    }
+    int fl = 0;
+    int iters = a.max_iter;
+    bool conv = false;
+    rows_pf(0);
+    for (int j = tid; j < n; j += TS) post[j] = L;      // (decoders.py:235-236)
+    for (int p = tid; p < a.E; p += TS) c2v[p] = 0.0;
+    for (int c0 = 64 * wid; c0 < m; c0 += TS) {
+      const int c = c0 + lane;
+      store_bits64(synw, c0, c < m ? (int)syn_bit(a, hs, c) : 0, lane);
+    }
+    __syncthreads();
+    // stop test after every layer by the parity filters (bp_team_kernel)
+    uint32_t bl = 0;
+    for (int c = lane; c < m; c += 64) bl ^= ((synw[c >> 5] >> (c & 31)) & 1u) ? a.wc[c] : 0u;
+    const uint32_t B = wave_xor(bl);
+    uint32_t F = (L < 0.0) ? a.filt_all : 0u;
+    uint32_t* fsl = red + 2 * W + 4;
+    for (int it = 0; it < a.max_iter && !conv; ++it) {
+      for (int l = 0; l < nl; ++l) {
+        const int q0 = lay_ptr[l], q1 = lay_ptr[l + 1];
+        const int v0 = adj_ptr[l], v1 = adj_ptr[l + 1];
+        uint32_t pa[NAF];                                 // this layer's adjacency, in flight during the CN
+#pragma unroll
+        for (int i = 0; i < NAF; ++i) {
+          const int q = v0 + TS * i + tid;
+          pa[i] = q < v1 ? adj_g[q] : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < NPF; ++i) {
+          if (q0 + GP * i < q1) {
+            const bool valid = q0 + GP * i + grp < q1;
+            const int c = (int)pc[i];
+            const uint32_t sb = valid ? (synw[c >> 5] >> (c & 31)) & 1u : 0u;
+            (void)cn_bp_word<DC>(a, pt[i], valid, k, lane, sb, post, c2v, fl);
+          }
+        }
+        for (int qb = q0 + GP * NPF; qb < q1; qb += GP) {  // layers of more than NPF passes
+          const int q = qb + grp;
+          const bool valid = q < q1;
+          const int c = valid ? (int)lrow_g[q] : 0;
+          const uint32_t t = (valid && k < DC) ? ltab_g[8 * q + k] : 0u;
+          const uint32_t sb = valid ? (synw[c >> 5] >> (c & 31)) & 1u : 0u;
+          (void)cn_bp_word<DC>(a, t, valid, k, lane, sb, post, c2v, fl);
+        }
+        rows_pf(l + 1 < nl ? l + 1 : 0);                  // in flight during the VN
+        __syncthreads();
+        uint32_t acc = 0;                                 // VN over the layer's adjacent variables
+        auto vn = [&](uint32_t info) {
+          const int j = (int)(info >> 21), d = (int)((info >> 16) & 31u);
+          const double old = post[j];
+          const double nw = d == 0 ? L : L + np_pairwise_sum(c2v + (info & 0xffffu), d);   // (:276-278)
+          post[j] = nw;
+          if ((old < 0.0) != (nw < 0.0)) acc ^= a.avar[j];
+        };
+#pragma unroll
+        for (int i = 0; i < NAF; ++i)
+          if (v0 + TS * i + tid < v1) vn(pa[i]);
+        for (int q = v0 + TS * NAF + tid; q < v1; q += TS) vn(adj_g[q]);
+        const uint32_t wacc = wave_xor(acc);
+        if (lane == 0) fsl[wid] = wacc;
+        __syncthreads();
+#pragma unroll
+        for (int w = 0; w < W; ++w) F ^= fsl[w];
+        if (F == B) {                                     // team-uniform
+          uint32_t un = 0;
+          for (int c = tid; c < m; c += TS) {
+            const uint4 t0 = *(const uint4*)(a.rtab + 8 * (size_t)c);
+            const uint4 t1 = *(const uint4*)(a.rtab + 8 * (size_t)c + 4);
+            const uint32_t rv[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+            uint32_t par = 0;
+#pragma unroll
+            for (int q = 0; q < DC; ++q) par ^= (uint32_t)(post[rv[q]] < 0.0);
+            un |= par ^ ((synw[c >> 5] >> (c & 31)) & 1u);
+          }
+          if (!team_any(un != 0)) {
+            iters = it + 1;
+            conv = true;
+            break;
+          }
+        }
+      }
+    }
+    double* po = a.post ? a.post + hs * (long long)n : nullptr;
+    for (int jo = tid; jo < n; jo += TS) {
+      const double pv = post[a.vinv[jo]];
+      put_ehat(a, hs, jo, pv < 0.0);                       // (:280)
+      if (po) po[jo] = pv;
+    }
+    const bool nonfin = team_any((fl & FLAG_NONFINITE) != 0);
+    if (tid == 0) {
+      a.iters[hs] = iters;
+      if (a.flags) a.flags[hs] = (int32_t)((nonfin ? FLAG_NONFINITE : 0) | (conv ? FLAG_CONVERGED : 0));
+      if (claimed) {
+        red[2 * W + 2 * tphase] = tk;
+        red[2 * W + 2 * tphase + 1] = tlen;
+      }
+    }
+    __syncthreads();                                      // slice reuse; ticket visible
+    if (!a.queue) {
+      hs += stride;
+    } else if (++hs >= end) {
+      const uint32_t t0 = red[2 * W + 2 * tphase], l0 = red[2 * W + 2 * tphase + 1];
+      tphase ^= 1;
+      seen = t0 + l0;
+      hs = stride + (long long)t0;
+      end = hs + l0;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Host-side launch helpers (called from capi.cpp)
 // ---------------------------------------------------------------------------
 template <int ALGO, bool LAYERED, int DC>
@@ -1991,6 +2187,14 @@ const void* select_bp_team_kernel(bool layered, int dc, int w, bool gt, const ch
     QLDPC_NAMED((&bp_team_kernel<L, D, Wn, true>), "bp_team_kernel<" #L ", " #D ", " #Wn ", true>");
   QLDPC_BPG(true, 7, 4) QLDPC_BPG(true, 8, 4) QLDPC_BPG(true, 7, 8) QLDPC_BPG(true, 8, 8)
 #undef QLDPC_BPG
+  return nullptr;
+}
+
+const void* select_bp_team_lg_kernel(int dc, int w, const char** name) {
+  if (dc == 7 && w == 4) QLDPC_NAMED((&bp_team_lg_kernel<7, 4>), "bp_team_lg_kernel<7, 4>");
+  if (dc == 8 && w == 4) QLDPC_NAMED((&bp_team_lg_kernel<8, 4>), "bp_team_lg_kernel<8, 4>");
+  if (dc == 7 && w == 8) QLDPC_NAMED((&bp_team_lg_kernel<7, 8>), "bp_team_lg_kernel<7, 8>");
+  if (dc == 8 && w == 8) QLDPC_NAMED((&bp_team_lg_kernel<8, 8>), "bp_team_lg_kernel<8, 8>");
   return nullptr;
 }
 

@@ -332,11 +332,13 @@ def test_ms_layered_irregular_columns_match_oracle(dec, sched):
 
 
 @pytest.mark.parametrize("code,w,gt", [("LP118_2", "4", "1"), ("LP118_2", "8", "1"), ("LP04_0", "4", "1"),
-                                        ("LP118_0", "8", "1"), ("LP118_2", "8", "0"), ("LP118_2", "4", "0")])
+                                        ("LP118_0", "8", "1"), ("LP118_2", "8", "0"), ("LP118_2", "4", "0"),
+                                        ("LP118_2", "4", "2"), ("LP04_0", "8", "2"), ("LP118_0", "4", "2")])
 def test_bp_team_global_row_table_matches_oracle(dec, code, w, gt, monkeypatch):
     """Layered BP teams with the row table in global memory and the compact
     LDS image (bp_team_kernel<true, DC, W, true>, QLDPC_BP_GT=1; LP118_2's
-    default) at both team widths, and the all-LDS team kernel (gt 0):
+    default) at both team widths, every table in global memory
+    (bp_team_lg_kernel, gt 2), and the all-LDS team kernel (gt 0):
     bit-exact vs the oracle on channel and fixed-work syndromes."""
     from oracle import oracle
     from qldpcsim_amd import _lib, codes, schedule
@@ -352,7 +354,10 @@ def test_bp_team_global_row_table_matches_oracle(dec, code, w, gt, monkeypatch):
     code_h._sched.clear()                  # launch configs read the env once per schedule
     try:
         nm = _lib.kernel_name(Hz, lp, lr, "BP")
-        assert nm.startswith("bp_team_kernel<true") and nm.endswith(f", {w}, true>" if gt == "1" else f", {w}>"), nm
+        if gt == "2":
+            assert nm.startswith("bp_team_lg_kernel<") and nm.endswith(f", {w}>"), nm
+        else:
+            assert nm.startswith("bp_team_kernel<true") and nm.endswith(f", {w}, true>" if gt == "1" else f", {w}, false>"), nm
         r = dec.decode_batch(Hz, syn, 0.08 / 3, 40, algo="BP", want_post=True, layer_ptr=lp, layer_rows=lr)
     finally:
         code_h._sched.clear()
