@@ -395,8 +395,11 @@ __device__ __forceinline__ int block_half_n(int SF, uint32_t (&lo)[SL], uint32_t
 // in VGPRs; RT = rows per thread (thread t holds rows t, t + blockDim, ..):
 // with 2, a 450-row shot takes 4 waves and a CU holds 4 shots (4 engines, one
 // per SIMD) instead of 2
+#ifndef QLDPC_OSD_WPE
+#define QLDPC_OSD_WPE 4  // waves per SIMD of the two-rows-per-thread instances (3: no spills, 15 % slower)
+#endif
 template <int NW, int SL, int RT>
-__global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_eu(RT == 2 ? 3 : 1))) osd_block_kernel(OsdArgs a) {
+__global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_eu(RT == 2 ? QLDPC_OSD_WPE : 1))) osd_block_kernel(OsdArgs a) {
   // LDS: inv_perm[n] | J list [m+2] | inJ bytes [n] | emask [NW] | Wd [MR] | Cm [MR] |
   //      PW [64][NW] | CT [64] | pkof [MR] | pidx [MR] | crow [MR] | pk [64] | misc [8] | set table
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
