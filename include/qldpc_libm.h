@@ -1,31 +1,41 @@
 /*
- * qldpc_libm.h — reproducible double-precision tanh / atanh for BP.
+ * qldpc_libm.h — NumPy's own float64 tanh / arctanh / log, restated bit for bit.
  *
- * BP_decoder (qLDPCsim/decoders.py:254-259) computes 2*atanh(prod/tanh(v/2)),
- * with atanh evaluated next to +-1 where it is ill-conditioned (|th2| up to
- * 1 - 1e-9): a one-ULP difference between two libms' tanh grows into ~1e-4
- * relative differences in converged posteriors. To make the GPU kernel and the
- * CPU oracle agree bit for bit, both evaluate these two functions with this
- * header: only IEEE-754 +, -, *, / and explicit fused multiply-add (each
- * correctly rounded on gfx950 — v_fma_f64 — and on x86-64 with FMA3; callers
- * compile with -ffp-contract=off so no other contraction happens, and the
- * host build needs -mfma so fma is the instruction, not glibc's emulation),
- * integer bit operations and comparisons. Accuracy against NumPy's
- * tanh/arctanh: <= 3 ULP over the BP domain (tests/test_libm.py).
+ * BP_decoder (qLDPCsim/decoders.py:254-259) computes
+ *     prod = np.prod(np.tanh(msgs / 2.0));  th2 = prod / np.tanh(v / 2.0)
+ *     val  = 2 * np.arctanh(th2)
+ * and both decoders start from L = np.log((1 - p) / max(p, eps)) (:147, :232).
+ * BP run for 100 iterations is chaotic: a last-bit difference in tanh or
+ * atanh grows into different hard decisions. So the GPU kernels and the CPU
+ * oracle evaluate exactly the functions NumPy evaluates on the reference's
+ * host (NumPy 2.2.6, x86-64 AVX512_SKX dispatch):
+ *   np.tanh    -> NumPy simd_tanh_f64 (loops_hyperbolic.dispatch.c.src):
+ *                 tanh(|x|) = Horner(c16 .. c0 of interval i)(|x| - b_i), the
+ *                 interval from the exponent and top 3 mantissa bits of x;
+ *   np.arctanh -> Intel SVML __svml_atanh8_ha (vendored by NumPy, BSD-3):
+ *                 0.5 (log(1+|x|) - log(1-|x|)) with each log reduced by a
+ *                 4-bit rounded reciprocal R (log(Y) = -log(R) + log1p(R Y - 1),
+ *                 R Y - 1 exact by FMA, two-term table of log(1 + i/16)) and
+ *                 one shared degree-9 series, summed with error terms;
+ *   np.log     -> Intel SVML __svml_log8_ha (host only: the prior L).
+ * The tables are NumPy's / SVML's own constants (include/qldpc_numpy_tables.h,
+ * generated from the installed NumPy by tools/gen_numpy_libm_tables.py). The
+ * SVML reciprocal is vrcp14pd rounded to a 4-bit mantissa; that rounded value
+ * is a step function of the top 18 mantissa bits, restated as 16 probed
+ * thresholds. Every other step is an IEEE-754 +, -, * or fused multiply-add
+ * in round-to-nearest, as in SVML's {rn-sae} code; callers compile with
+ * -ffp-contract=off (no other contraction) and the host build with -mfma.
+ * tests/test_libm.py checks the three functions against NumPy itself.
  *
- * Method: tanh = e/(e+2), e = expm1(2|x|) (Cody–Waite reduction y = k ln2 + r,
- * |r| <= ln2/2, degree-14 Taylor polynomial, 2^k (1 + expm1 r) - 1
- * reassembled exactly); atanh(a) = k ln2/2 + atanh(s), s = (N - D 2^k) /
- * (N + D 2^k) with N = 1 + a and D = 1 - a held as exact two-term sums and
- * 2^k the power of two nearest N / D (|s| <= 3 - 2 sqrt2; odd series in s).
- * One division each and no data-dependent branches below the special values,
- * because GPU lanes diverge (atanh: 133 -> ~60 gfx950 instructions; fewer
- * 2-3 ULP cases than the fdlibm log1p form it replaced).
+ * Table image: host code reads qldpc_libm_host; device kernels stage the same
+ * image (qldpc_libm_tab) into LDS and pass pointers into it.
  */
 #ifndef QLDPC_LIBM_H
 #define QLDPC_LIBM_H
 
 #include <stdint.h>
+
+#include "qldpc_numpy_tables.h"
 
 #if defined(__HIPCC__) || defined(__HIP__)
 #define QLDPC_HD __host__ __device__ __forceinline__
@@ -57,12 +67,13 @@ __device__ __forceinline__ double qldpc_fma_dev(double a, double b, double c) {
   return r;
 }
 #define QLDPC_FMA(a, b, c) qldpc_fma_dev((a), (b), (c))
-/* a / b correctly rounded, for finite b != 0 and operands whose exponents lie
-   well inside the normal range (here: 2^-500 < |a|, |b| < 2^500, or a == 0).
-   It is the compiler's IEEE division sequence (v_rcp_f64, two Newton steps,
-   q = a r, one FMA correction) without v_div_scale / v_div_fixup, which are the
-   identity in that range: the same result, bit for bit, in 8 instead of 11
-   VALU ops. Callers guarantee the range. */
+/* a / b correctly rounded, for finite b != 0 and NONZERO a, both well inside
+   the normal range (2^-500 < |a|, |b| < 2^500). It is the compiler's IEEE
+   division sequence (v_rcp_f64, two Newton steps, q = a r, one FMA
+   correction) without v_div_scale / v_div_fixup, which are the identity in
+   that range: the same result, bit for bit, in 8 instead of 11 VALU ops.
+   (a = -0 would come out +0: v_div_fixup is what sets that sign.) Callers
+   guarantee the range. */
 __device__ __forceinline__ double qldpc_div_dev(double a, double b) {
   double r = __builtin_amdgcn_rcp(b);
   double e = qldpc_fma_dev(-b, r, 1.0);
@@ -79,156 +90,163 @@ __device__ __forceinline__ double qldpc_div_dev(double a, double b) {
 #define QLDPC_DIV(a, b) ((a) / (b))
 #endif
 
-#define QLDPC_LN2_HI 6.93147180369123816490e-01 /* 0x3fe62e42fee00000: k*LN2_HI exact for |k| < 2^11 */
-#define QLDPC_LN2_LO 1.90821492927058770002e-10 /* 0x3dea39ef35793c76 */
-#define QLDPC_INV_LN2 1.44269504088896338700e+00
+/* the table image: NumPy's tanh intervals [16][18] (b, c0 .. c16), SVML
+   atanh's log(1 + i/16) [16][2] (hi, lo) and its reciprocal step buckets */
+typedef struct {
+  double tanh_c[16 * 18];
+  double atanh_hl[16 * 2];
+  uint32_t atanh_rcp[64];
+} qldpc_libm_tab;
 
-/* e^r - 1 for |r| <= ln2/2 (+ a little): r + r^2 * sum_{k>=2} r^(k-2)/k!
-   (Horner with fused multiply-adds) */
-QLDPC_HD double qldpc_expm1_small(double r) {
-  double q = 1.0 / 87178291200.0;                 /* 1/14! */
-  q = QLDPC_FMA(q, r, 1.0 / 6227020800.0);        /* 1/13! */
-  q = QLDPC_FMA(q, r, 1.0 / 479001600.0);         /* 1/12! */
-  q = QLDPC_FMA(q, r, 1.0 / 39916800.0);          /* 1/11! */
-  q = QLDPC_FMA(q, r, 1.0 / 3628800.0);           /* 1/10! */
-  q = QLDPC_FMA(q, r, 1.0 / 362880.0);            /* 1/9!  */
-  q = QLDPC_FMA(q, r, 1.0 / 40320.0);             /* 1/8!  */
-  q = QLDPC_FMA(q, r, 1.0 / 5040.0);              /* 1/7!  */
-  q = QLDPC_FMA(q, r, 1.0 / 720.0);               /* 1/6!  */
-  q = QLDPC_FMA(q, r, 1.0 / 120.0);               /* 1/5!  */
-  q = QLDPC_FMA(q, r, 1.0 / 24.0);                /* 1/4!  */
-  q = QLDPC_FMA(q, r, 1.0 / 6.0);                 /* 1/3!  */
-  q = QLDPC_FMA(q, r, 0.5);                       /* 1/2!  */
-  return QLDPC_FMA(r * r, q, r);
+#define QLDPC_LIBM_TAB_INIT { QLDPC_TANH_LUT_INIT, QLDPC_ATANH_HL_INIT, QLDPC_ATANH_RCP_INIT }
+
+/* np.tanh (NumPy simd_tanh_f64). tc = qldpc_libm_tab.tanh_c. */
+QLDPC_HD double qldpc_tanh_t(double x, const double* tc) {
+  const uint64_t u = qldpc_d2bits(x);
+  const uint64_t nd = u & 0x7ff8000000000000ull;      /* exponent + top 3 mantissa bits */
+  int32_t h = (int32_t)(uint32_t)(nd >> 32) - 0x3fc00000;
+  h = h < 0 ? 0 : h;
+  h = h > 0x780000 ? 0x780000 : h;
+  const double* c = tc + 18 * (h >> 19);              /* interval 0 .. 15 */
+  const double y = qldpc_bits2d(u & 0x7fffffffffffffffull) - c[0];
+  double r = c[17];
+  r = QLDPC_FMA(r, y, c[16]);
+  r = QLDPC_FMA(r, y, c[15]);
+  r = QLDPC_FMA(r, y, c[14]);
+  r = QLDPC_FMA(r, y, c[13]);
+  r = QLDPC_FMA(r, y, c[12]);
+  r = QLDPC_FMA(r, y, c[11]);
+  r = QLDPC_FMA(r, y, c[10]);
+  r = QLDPC_FMA(r, y, c[9]);
+  r = QLDPC_FMA(r, y, c[8]);
+  r = QLDPC_FMA(r, y, c[7]);
+  r = QLDPC_FMA(r, y, c[6]);
+  r = QLDPC_FMA(r, y, c[5]);
+  r = QLDPC_FMA(r, y, c[4]);
+  r = QLDPC_FMA(r, y, c[3]);
+  r = QLDPC_FMA(r, y, c[2]);
+  r = QLDPC_FMA(r, y, c[1]);
+  r = nd <= 0x7fe0000000000000ull ? r : 1.0;         /* |x| >= 2^1023, inf */
+  r = qldpc_bits2d(qldpc_d2bits(r) | (u & 0x8000000000000000ull));
+  return (x == x) ? r : qldpc_bits2d(0x7ff8000000000000ull);
 }
 
-/* e^y - 1 for 0 <= y <= 64 */
-QLDPC_HD double qldpc_expm1_pos(double y) {
-  const int k = (int)(y * QLDPC_INV_LN2 + 0.5);
-  const double fk = (double)k;
-  const double r = QLDPC_FMA(-fk, QLDPC_LN2_LO, y - fk * QLDPC_LN2_HI);  /* fk*LN2_HI exact */
-  const double em = qldpc_expm1_small(r);
-  const double two_k = qldpc_bits2d((uint64_t)(k + 1023) << 52);
-  return QLDPC_FMA(two_k, em, two_k - 1.0);      /* two_k - 1 exact for k <= 53; k = 0: em */
+/* vrcp14pd(Y) rounded half-up to a 4-bit mantissa (SVML atanh), for a
+   positive normal Y: R = 2^-e (1 - c/32) with c = the number of probed steps
+   at or below Y's mantissa (bucketed by its top 6 bits); *ge = getexp(R). */
+QLDPC_HD double qldpc_svml_rrcp(double Y, const uint32_t* rb, double* ge, int* ti) {
+  const uint64_t u = qldpc_d2bits(Y);
+  const int e = (int)((u >> 52) & 0x7ff) - 1023;
+  const uint32_t p = (uint32_t)(u >> 34) & 0x3ffffu;
+  const uint32_t ent = rb[p >> 12];
+  const int c = (int)(ent & 0xffu) + (p >= (ent >> 8) ? 1 : 0);
+  *ge = (double)((c == 0 ? 0 : -1) - e);
+  *ti = (16 - c) & 15;                                 /* table index = R's top mantissa bits */
+  return qldpc_bits2d(((uint64_t)(0x3ff0 - c) << 48) + ((uint64_t)(int64_t)(-e) << 52));
 }
 
-QLDPC_HD double qldpc_tanh(double x) {
-  const uint64_t sgn = qldpc_d2bits(x) & 0x8000000000000000ull;
-  const double a = qldpc_bits2d(qldpc_d2bits(x) & 0x7fffffffffffffffull);
-  if (!(a == a)) return x;                        /* NaN */
-  /* branch-free (lanes diverge): the range cases are selects */
-  const double ac = a < 22.0 ? a : 22.0;
-  const double em = qldpc_expm1_pos(ac + ac);
-  double t = QLDPC_DIV(em, em + 2.0);             /* one division (<= 3 ULP); em + 2 in [2, 2^64],
-                                                     em = 0 or > 2^-500 where t is kept */
-  t = a >= 22.0 ? 1.0 : t;                        /* 1 - tanh(22) < 2^-62 */
-  t = a < 3.7252902984e-09 ? a : t;               /* 2^-28: tanh(x) = x in double */
-  return qldpc_bits2d(qldpc_d2bits(t) | sgn);
+/* np.arctanh (SVML __svml_atanh8_ha). hl = qldpc_libm_tab.atanh_hl, rb =
+   .atanh_rcp. |x| >= 1 and NaN take SVML's rare path: +-inf at |x| == 1,
+   NaN otherwise (signs / payloads as below; BP flags them non-finite). */
+QLDPC_HD double qldpc_atanh_t(double x, const double* hl, const uint32_t* rb) {
+  const uint64_t u = qldpc_d2bits(x);
+  const uint64_t sgn = u & 0x8000000000000000ull;
+  const double ax = qldpc_bits2d(u & 0x7fffffffffffffffull);
+  if (!(ax == ax)) return x;
+  if (ax >= 1.0) return qldpc_bits2d(((ax == 1.0) ? 0x7ff0000000000000ull : 0x7ff8000000000000ull) | sgn);
+  const double Yp = ax + 1.0, Ym = 1.0 - ax;
+  const double Yp_lo = ax - (Yp - 1.0);                /* 1 + ax = Yp + Yp_lo */
+  const double Ym_nlo = ax + (Ym - 1.0);               /* 1 - ax = Ym - Ym_nlo */
+  double gp, gm;
+  int ip, im;
+  const double Rp = qldpc_svml_rrcp(Yp, rb, &gp, &ip);
+  const double Rm = qldpc_svml_rrcp(Ym, rb, &gm, &im);
+  const double dp = QLDPC_FMA(Yp_lo, Rp, QLDPC_FMA(Rp, Yp, -1.0));   /* Rp (1 + ax) - 1 */
+  const double dm = QLDPC_FMA(-Ym_nlo, Rm, QLDPC_FMA(Ym, Rm, -1.0)); /* Rm (1 - ax) - 1 */
+  const double ediff = gm - gp;
+  double Pp = QLDPC_FMA(QLDPC_ATANH_C0, dp, QLDPC_ATANH_C1);
+  double Pm = QLDPC_FMA(QLDPC_ATANH_C0, dm, QLDPC_ATANH_C1);
+  const double K = QLDPC_FMA(QLDPC_ATANH_LN2HI, ediff, hl[2 * im] - hl[2 * ip]);
+  Pp = QLDPC_FMA(dp, Pp, QLDPC_ATANH_C2);
+  Pm = QLDPC_FMA(dm, Pm, QLDPC_ATANH_C2);
+  Pp = QLDPC_FMA(dp, Pp, QLDPC_ATANH_C3);
+  Pm = QLDPC_FMA(dm, Pm, QLDPC_ATANH_C3);
+  const double Klo = QLDPC_FMA(QLDPC_ATANH_LN2LO, ediff, hl[2 * im + 1] - hl[2 * ip + 1]);
+  const double dp2 = dp * dp;
+  Pp = QLDPC_FMA(dp, Pp, QLDPC_ATANH_C4);
+  Pm = QLDPC_FMA(dm, Pm, QLDPC_ATANH_C4);
+  const double S1 = dp + K;
+  Pp = QLDPC_FMA(dp, Pp, QLDPC_ATANH_C5);
+  Pm = QLDPC_FMA(dm, Pm, QLDPC_ATANH_C5);
+  const double dm2 = dm * dm;
+  Pp = QLDPC_FMA(dp, Pp, QLDPC_ATANH_C6);
+  Pm = QLDPC_FMA(dm, Pm, QLDPC_ATANH_C6);
+  const double t4 = K - S1;
+  const double S2 = S1 - dm;
+  Pp = QLDPC_FMA(dp, Pp, QLDPC_ATANH_C7);
+  Pm = QLDPC_FMA(dm, Pm, QLDPC_ATANH_C7);
+  Pp = QLDPC_FMA(dp, Pp, QLDPC_ATANH_C8);
+  Pm = QLDPC_FMA(dm, Pm, QLDPC_ATANH_C8);
+  const double e1 = dp + t4;                           /* rounding error of S1 */
+  const double t5 = S2 - S1;
+  const double A = QLDPC_FMA(dp2, Pp, Klo);
+  const double B = QLDPC_FMA(-dm2, Pm, e1);
+  const double e2 = dm + t5;                           /* (minus) rounding error of S2 */
+  const double r = S2 + ((A + B) - e2);
+  return r * qldpc_bits2d(0x3fe0000000000000ull | sgn);   /* +-0.5 */
 }
 
-/* log(1 + f) for f > -1 */
-QLDPC_HD double qldpc_log1p(double f) {
-  if (!(f == f)) return f;
-  if (f <= -1.0) return (f == -1.0) ? -qldpc_bits2d(0x7ff0000000000000ull) : qldpc_bits2d(0x7ff8000000000000ull);
-  const double af = f < 0 ? -f : f;
-  if (af < 5.551115123125783e-17) return f;        /* 2^-54 */
-  if (f == qldpc_bits2d(0x7ff0000000000000ull)) return f;
-  int k = 0;
-  double fm = f, c = 0.0;
-  if (!(f > -0.2928932188134524 && f < 0.41421356237309503)) {
-    /* u = 1 + f = 2^k m, m in [sqrt2/2, sqrt2); c = rounding error of u,
-       relative to u (fdlibm's c). Inside (1/sqrt2 - 1, sqrt2 - 1), k = 0 and
-       f itself is the reduced argument (no rounding, no correction). */
-    const double u = 1.0 + f;
-    const uint64_t ub = qldpc_d2bits(u);
-    k = (int)((ub >> 52) & 0x7ff) - 1023;
-    uint64_t mb = (ub & 0x000fffffffffffffull) | 0x3ff0000000000000ull;   /* m in [1, 2) */
-    if (mb > 0x3ff6a09e667f3bcdull) {                                     /* m > sqrt(2) */
-      mb = (mb & 0x000fffffffffffffull) | 0x3fe0000000000000ull;          /* m / 2 */
-      k += 1;
-    }
-    fm = qldpc_bits2d(mb) - 1.0;                   /* exact (Sterbenz) */
-    if (k < 54) {
-      /* c / u needs ~1e-6 relative accuracy only (|c/u| <= 2^-53 here and
-         the result is >= 0.34): multiply by a three-step Newton reciprocal of
-         the mantissa instead of dividing. */
-      const double cc = (k > 0) ? 1.0 - (u - f) : f - (u - 1.0);
-      const double mu = qldpc_bits2d((ub & 0x000fffffffffffffull) | 0x3ff0000000000000ull);  /* [1,2) */
-      double r = 1.4571067811865475 - 0.5 * mu;     /* |r - 1/mu| < 0.09 */
-      r = r * QLDPC_FMA(-mu, r, 2.0);
-      r = r * QLDPC_FMA(-mu, r, 2.0);
-      r = r * QLDPC_FMA(-mu, r, 2.0);
-      const double two_mk = qldpc_bits2d((uint64_t)(1023 - ((int)((ub >> 52) & 0x7ff) - 1023)) << 52);
-      c = cc * r * two_mk;
-    }
-  }
-  const double s = fm / (2.0 + fm);
-  const double z = s * s;
-  double R = 2.0 / 25.0;
-  R = QLDPC_FMA(R, z, 2.0 / 23.0);
-  R = QLDPC_FMA(R, z, 2.0 / 21.0);
-  R = QLDPC_FMA(R, z, 2.0 / 19.0);
-  R = QLDPC_FMA(R, z, 2.0 / 17.0);
-  R = QLDPC_FMA(R, z, 2.0 / 15.0);
-  R = QLDPC_FMA(R, z, 2.0 / 13.0);
-  R = QLDPC_FMA(R, z, 2.0 / 11.0);
-  R = QLDPC_FMA(R, z, 2.0 / 9.0);
-  R = QLDPC_FMA(R, z, 2.0 / 7.0);
-  R = QLDPC_FMA(R, z, 2.0 / 5.0);
-  R = QLDPC_FMA(R, z, 2.0 / 3.0);
-  R = R * z;
-  const double hfsq = 0.5 * fm * fm;
-  const double fk = (double)k;
-  return QLDPC_FMA(fk, QLDPC_LN2_HI, (fm - QLDPC_FMA(-s, hfsq + R, hfsq)) + QLDPC_FMA(fk, QLDPC_LN2_LO, c));
+/* host image of the tables (the oracle, the library's host code; in HIP
+   sources these are host functions, never emitted for the device) */
+static const qldpc_libm_tab qldpc_libm_host = QLDPC_LIBM_TAB_INIT;
+static const uint64_t qldpc_log_rcp_t[16] = QLDPC_LOG_RCP_T_INIT;
+static const double qldpc_log_ab[32] = QLDPC_LOG_AB_INIT;
+
+static inline double qldpc_tanh(double x) { return qldpc_tanh_t(x, qldpc_libm_host.tanh_c); }
+static inline double qldpc_atanh(double x) {
+  return qldpc_atanh_t(x, qldpc_libm_host.atanh_hl, qldpc_libm_host.atanh_rcp);
 }
 
-/* atanh(s) for |s| <= 0.1716: s + s^3 (1/3 + s^2/5 + ... + s^20/21)
-   (first omitted term < 2^-60 |s|) */
-QLDPC_HD double qldpc_atanh_small(double s) {
-  const double z = s * s;
-  double q = 1.0 / 21.0;
-  q = QLDPC_FMA(q, z, 1.0 / 19.0);
-  q = QLDPC_FMA(q, z, 1.0 / 17.0);
-  q = QLDPC_FMA(q, z, 1.0 / 15.0);
-  q = QLDPC_FMA(q, z, 1.0 / 13.0);
-  q = QLDPC_FMA(q, z, 1.0 / 11.0);
-  q = QLDPC_FMA(q, z, 1.0 / 9.0);
-  q = QLDPC_FMA(q, z, 1.0 / 7.0);
-  q = QLDPC_FMA(q, z, 1.0 / 5.0);
-  q = QLDPC_FMA(q, z, 1.0 / 3.0);
-  return QLDPC_FMA(s * z, q, s);
+/* np.log (SVML __svml_log8_ha) for positive normal finite x; other inputs
+   (0, negative, subnormal, inf, NaN — SVML's rare path) return NaN, -inf or
+   the input as IEEE log does. The prior L = log((1-p)/max(p, eps)) only
+   ever sees finite positive normal arguments. */
+static inline double qldpc_np_log(double x) {
+  const uint64_t u = qldpc_d2bits(x);
+  const int ex = (int)((u >> 52) & 0x7ff);
+  if (x != x || x < 0.0) return qldpc_bits2d(0x7ff8000000000000ull);
+  if (x == 0.0) return -qldpc_bits2d(0x7ff0000000000000ull);
+  if (ex == 0x7ff) return x;
+  if (ex == 0) return qldpc_bits2d(0x7ff8000000000000ull);   /* subnormal: not restated */
+  double e = (double)(ex - 1023);
+  const uint64_t mb = u & 0x000fffffffffffffull;
+  const double m = qldpc_bits2d(mb | 0x3ff0000000000000ull);            /* getmant [1, 2) */
+  int c = 0;
+  for (int k = 0; k < 16; ++k) c += mb >= qldpc_log_rcp_t[k];
+  const double R = qldpc_bits2d((uint64_t)(0x3ff0 - c) << 48);          /* vrndscale(vrcp14(m), 2^-5) */
+  const int idx = (16 - c) & 15;
+  const double r = __builtin_fma(R, m, -QLDPC_LOG_C100);
+  const double A1 = __builtin_fma(QLDPC_LOG_C200, r, QLDPC_LOG_C240);
+  const double A0 = __builtin_fma(QLDPC_LOG_C180, r, QLDPC_LOG_C1c0);
+  const double r2 = r * r;
+  const double A2 = __builtin_fma(QLDPC_LOG_C280, r, QLDPC_LOG_C2c0);
+  const double B0 = __builtin_fma(r2, A0, A1);
+  const double r4 = r2 * r2;
+  const double A3 = __builtin_fma(QLDPC_LOG_C300, r, QLDPC_LOG_C340);
+  if (R < QLDPC_LOG_C140) e = e + QLDPC_LOG_C100;
+  const double B1 = __builtin_fma(r2, A2, A3);
+  const double H = __builtin_fma(QLDPC_LOG_C380, e, qldpc_log_ab[2 * idx]);
+  const double P = __builtin_fma(r4, B0, B1);
+  const double S = H + r;
+  const double err = r - (S - H);
+  const double Q = __builtin_fma(r2, P, err);
+  const double E2 = __builtin_fma(QLDPC_LOG_C3c0, e, qldpc_log_ab[2 * idx + 1]);
+  return S + (Q + E2);
 }
 
-/* atanh(a) = atanh(s) + k ln2 / 2 with s = (N - D 2^k) / (N + D 2^k),
-   N = 1 + a, D = 1 - a (ratio of the two = 2^k m, m in [sqrt2/2, sqrt2],
-   so |s| <= 3 - 2 sqrt2). N and D are carried as exact two-term sums (their
-   rounding errors by Fast2Sum), N - D 2^k is exact (Sterbenz) and the
-   corrections enter once: one division in all, no logarithm. Below
-   3 - 2 sqrt2, k = 0 and s = a exactly. */
-QLDPC_HD double qldpc_atanh(double x) {
-  const uint64_t sgn = qldpc_d2bits(x) & 0x8000000000000000ull;
-  const double a = qldpc_bits2d(qldpc_d2bits(x) & 0x7fffffffffffffffull);
-  if (!(a == a)) return x;
-  if (a >= 1.0)
-    return qldpc_bits2d(((a == 1.0) ? 0x7ff0000000000000ull : 0x7ff8000000000000ull) | sgn);
-  /* branch-free below 1 (lanes diverge): both ranges share one series */
-  const double N = 1.0 + a, eN = (1.0 - N) + a;    /* N + eN = 1 + a exactly */
-  const double D = 1.0 - a, eD = (1.0 - D) - a;    /* D + eD = 1 - a exactly */
-  /* k = round(log2(N / D)): N in [1, 2); D = 2^-e mD, mD in [1, 2) */
-  const uint64_t db = qldpc_d2bits(D);
-  int k = 1023 - (int)((db >> 52) & 0x7ff);         /* e */
-  const double mD = qldpc_bits2d((db & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
-  if (N > 1.4142135623730951 * mD) k += 1;          /* N / (D 2^k) into [sqrt2/2, sqrt2] */
-  const double p2k = qldpc_bits2d((uint64_t)(1023 + k) << 52);
-  const double Dk = D * p2k, eDk = eD * p2k;        /* exact */
-  const double num = (N - Dk) + (eN - eDk);         /* N - Dk exact (Sterbenz) */
-  const double den = (N + Dk) + (eN + eDk);
-  const int big = a > 0.17157287525381;             /* 3 - 2 sqrt2 (rounded down) */
-  const double sr = big ? QLDPC_DIV(num, den) : a; /* below: k = 0, s = a exactly; den in [1, 4],
-                                                     num = 0 or |num| > 2^-110 where big */
-  const double fk = big ? (double)k : 0.0;
-  const double t = QLDPC_FMA(fk, 0.5 * QLDPC_LN2_HI, qldpc_atanh_small(sr) + fk * (0.5 * QLDPC_LN2_LO));
-  return qldpc_bits2d(qldpc_d2bits(t) | sgn);
+/* L_ch = np.log((1 - p) / max(p, eps))   (decoders.py:147, :232) */
+static inline double qldpc_prior_llr(double p, double eps) {
+  return qldpc_np_log((1.0 - p) / (p > eps ? p : eps));
 }
 
 #endif /* QLDPC_LIBM_H */

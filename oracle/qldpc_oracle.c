@@ -22,10 +22,11 @@
  *   BP: float64; product of tanh = sequential fold (np.prod, :254); division
  *       extrinsic (:256); eps clip (:257-258); column sums follow NumPy's
  *       pairwise_sum (0.0 + pairwise(all), 8-accumulator blocks for n >= 8,
- *       :269/:276). tanh/atanh come from include/qldpc_libm.h (<= 3 ULP from
- *       NumPy's), the same code the GPU kernel runs, so GPU and oracle agree
- *       bit for bit while oracle and reference agree to ULP level (BP's atanh
- *       near +-1 amplifies any libm difference; see that header).
+ *       :269/:276). tanh/atanh (and, for both decoders, the log of the prior)
+ *       come from include/qldpc_libm.h: NumPy's own float64 tanh and SVML's
+ *       atanh / log as NumPy runs them on the reference's host, restated bit
+ *       for bit — the same code the GPU kernels run, so GPU, oracle and
+ *       reference agree bit for bit, 100-iteration chaotic decodes included.
  * Build: oracle/Makefile  ->  oracle/_build/libqldpc_oracle.so
  */
 #include <math.h>
@@ -33,7 +34,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include "../include/qldpc_libm.h" /* reproducible tanh/atanh, shared with the GPU kernel */
+#include "../include/qldpc_libm.h" /* NumPy-exact tanh/atanh/log, shared with the GPU kernels */
 
 #define ORACLE_FLAG_MIN_ZERO 1  /* MS: a check saw min|v| == 0 (App. A.1.6 leak case, not emulated) */
 #define ORACLE_FLAG_NONFINITE 2 /* BP: tanh(v/2)==0 or a non-finite message */
@@ -80,7 +81,7 @@ static int ms_decode_one(const graph_t *g, const uint8_t *syn, double p, int max
                          double beta, double eps, uint8_t *ehat, double *post_out,
                          int *flags, float *c2v, float *c2v_new, float *S, double *post) {
     const int n = g->n;
-    const double L = log((1.0 - p) / (p > eps ? p : eps));  /* :147 (np.float64) */
+    const double L = qldpc_prior_llr(p, eps);               /* :147 np.log (np.float64) */
     const float L32 = (float)L;                              /* :148-149 float32 store */
     for (int e = 0; e < g->E; ++e) c2v[e] = 0.0f;           /* :150 */
     for (int j = 0; j < n; ++j) { S[j] = 0.0f; post[j] = L + (double)0.0f; }
@@ -172,7 +173,7 @@ static int bp_decode_one(const graph_t *g, const uint8_t *syn, double p, int max
                          double eps, uint8_t *ehat, double *post_out, int *flags,
                          double *v2c, double *c2v, double *tmp, double *post) {
     const int n = g->n;
-    const double L0 = log((1.0 - p) / (p > eps ? p : eps));  /* :232 */
+    const double L0 = qldpc_prior_llr(p, eps);              /* :232 np.log */
     for (int e = 0; e < g->E; ++e) { v2c[e] = L0; c2v[e] = 0.0; }  /* :235-236 */
     *flags = 0;
     for (int it = 0; it < max_iter; ++it) {

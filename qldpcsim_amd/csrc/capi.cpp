@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "../../include/qldpc_decoder.h"
+#include "../../include/qldpc_libm.h"
 #include "decoder_kernels.h"
 #include "osd_kernels.h"
 #include "channel_kernels.h"
@@ -246,11 +247,8 @@ struct LaunchCfg {
   int waves = 0, blocks_per_cu = 0, lds = 0, wave_bytes = 0;
   bool lblob = false;  // uses the layer-ordered blob (ms_layered_kernel)
   bool gtab = false;     // ms_flood_kernel: global tables, LDS = wave state only
-  bool tgt = false;      // bp_team_kernel<.., true>: row table global, LDS image = tblob
   bool tlg = false;      // bp_team_lg_kernel: every table global, LDS image = layer pointers
   int team = 0;          // bp_team_kernel: waves per half-shot (one workgroup), 0 = wave kernels
-  int nh = 1;            // ms_layered_grp_kernel: half-shots per wave
-  int slice = 0;         // ms_layered_grp_kernel: bytes of one half-shot's LDS slice
   const char* name = "";  // kernel name as rocprofv3 reports it
   bool ok = false;
 };
@@ -270,17 +268,11 @@ struct qldpc_schedule {
   int off_cn_tab = 0, off_row_ptr = 0, off_vn_ptr = 0, off_vn_chk = 0;
   int off_lay_ptr = 0, off_lay_rows = 0, off_adj_ptr = 0, off_adj_vars = 0, off_chunk_dmax = 0;
   unsigned char* d_blob = nullptr;
-  // layered BP teams (bp_team_kernel<true, DC, W, true>): variable and layer
-  // tables first (the LDS image), then the row table read from global memory
-  std::vector<uint8_t> tblob;
-  unsigned char* d_tblob = nullptr;
   // layered BP teams with every table global (bp_team_lg_kernel): layer
   // pointers (the LDS image), then rows in layer order, their checks, adjacency
   std::vector<uint8_t> lgblob;
   unsigned char* d_lgblob = nullptr;
   int lg_lds_bytes = 0, lg_off_lay_ptr = 0, lg_off_adj_ptr = 0, lg_off_ltab = 0, lg_off_lrow = 0, lg_off_adj = 0;
-  int t_lds_bytes = 0, t_off_cn_tab = 0, t_off_vn_ptr = 0, t_off_lay_ptr = 0, t_off_lay_rows = 0,
-      t_off_adj_ptr = 0, t_off_adj_vars = 0;
   // flooding MS, uniform degree: global table image of ms_flood_kernel
   std::vector<uint8_t> fblob;
   unsigned char* d_fblob = nullptr;
@@ -399,17 +391,6 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
       std::sort(rows.begin(), rows.end());
       s->median_rows = n_layers ? rows[n_layers / 2] : 0;
     }
-    if (fast_table_ok(code)) {
-      s->t_off_vn_ptr = put(s->tblob, vn_ptr);
-      s->t_off_lay_ptr = put(s->tblob, lay_ptr);
-      s->t_off_lay_rows = put(s->tblob, lay_rows);
-      s->t_off_adj_ptr = put(s->tblob, adj_ptr);
-      s->t_off_adj_vars = put(s->tblob, adj_vars);
-      s->tblob.resize(align16((int)s->tblob.size() + 1));
-      s->t_lds_bytes = (int)s->tblob.size();
-      s->t_off_cn_tab = put(s->tblob, cn_tab);
-      s->tblob.resize(align16((int)s->tblob.size() + 1));
-    }
     s->off_vn_chk = put(s->blob, vn_chk);
     s->off_lay_ptr = put(s->blob, lay_ptr);
     s->off_lay_rows = put(s->blob, lay_rows);
@@ -432,12 +413,11 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
       // bits 5-6: log2 of the layer's lanes per check (ms_layered_kernel<DC, 0>):
       // one lane per check for long layers, a lane group when the layer leaves
       // most of the wave idle (rows <= 8: 8 lanes, <= 16: 4)
+      // (two lanes per check on 17-64-row layers measured 5-12 % slower, round 2)
       s->layer_g = -2;
-      int g2_rows = 16;   // rows in (16, g2_rows]: 2 lanes per check
-      if (const char* ev = getenv("QLDPC_MS_G2_ROWS")) g2_rows = atoi(ev);
       for (int l = 0; l < n_layers; ++l) {
         const int rows = lay_ptr[l + 1] - lay_ptr[l];
-        const int gl = rows <= 8 ? 3 : (rows <= 16 ? 2 : (rows <= g2_rows ? 1 : 0));
+        const int gl = rows <= 8 ? 3 : (rows <= 16 ? 2 : 0);
         adj_dmax[l] = (uint8_t)(adj_dmax[l] | (gl << 5));
         s->layer_g = (s->layer_g == -2 || s->layer_g == (1 << gl)) ? (1 << gl) : 0;
       }
@@ -517,10 +497,6 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
     e1 = hipMalloc(&s->d_lgblob, s->lgblob.size());
     if (e1 == hipSuccess) e1 = hipMemcpy(s->d_lgblob, s->lgblob.data(), s->lgblob.size(), hipMemcpyHostToDevice);
   }
-  if (e1 == hipSuccess && !s->tblob.empty()) {
-    e1 = hipMalloc(&s->d_tblob, s->tblob.size());
-    if (e1 == hipSuccess) e1 = hipMemcpy(s->d_tblob, s->tblob.data(), s->tblob.size(), hipMemcpyHostToDevice);
-  }
   if (e1 == hipSuccess && !s->lblob.empty()) {
     e1 = hipMalloc(&s->d_lblob, s->lblob.size());
     if (e1 == hipSuccess) e1 = hipMemcpy(s->d_lblob, s->lblob.data(), s->lblob.size(), hipMemcpyHostToDevice);
@@ -537,7 +513,6 @@ extern "C" int qldpc_schedule_destroy(qldpc_schedule* s) {
   if (!s) return QLDPC_OK;
   (void)hipFree(s->d_blob);
   (void)hipFree(s->d_lblob);
-  (void)hipFree(s->d_tblob);
   (void)hipFree(s->d_lgblob);
   (void)hipFree(s->d_fblob);
   (void)hipFree(s->d_queue);
@@ -557,16 +532,6 @@ static void wave_layout(const qldpc_code* c, bool layered, int algo, int* bytes,
   *off_parw = off;
   if (layered && !colsum_f32) off = align16(off + 4 * words);  // ms_layered_kernel: filters, no parity words
   *bytes = std::max(off, 16);
-}
-
-// ms_layered_grp_kernel's per-half-shot slice: colS f32[n] | c2v f32[E + 8] | syndrome u8[m]
-static void grp_layout(const qldpc_code* c, int* bytes, int* off_c2v, int* off_synb) {
-  int off = align16(4 * c->n);
-  *off_c2v = off;
-  off = align16(off + 4 * (c->E + 8));
-  *off_synb = off;
-  off = align16(off + c->m);
-  *bytes = off;
 }
 
 // bp_team_kernel's slice: post f64[n] | c2v f64[E + 8] | syn words | parity
@@ -612,18 +577,9 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
     // else chosen per layer (the runtime switch costs ~5 % where it is not needed)
     int g = s->layer_g > 0 ? s->layer_g : 0;
     if (const char* ev = getenv("QLDPC_MS_LANES_PER_CHECK")) g = atoi(ev);
-    // ms_layered_grp_kernel (several half-shots per wave) only on request:
-    // at a fixed LDS budget it halves the waves per CU, and the layered
-    // kernels are latency-bound (interleaved A/B: LP118_2 MS-L 35 -> 75 ms)
-    int nh = 1;
-    if (const char* ev = getenv("QLDPC_MS_GROUPS")) nh = atoi(ev);
-    if (nh > 1 || getenv("QLDPC_MS_GRP_G")) {
-      int gg = (s->median_rows * 2 <= 64 / nh) ? 2 : 1;
-      if (const char* ev = getenv("QLDPC_MS_GRP_G")) gg = atoi(ev);
-      cfg.kernel = qldpc::select_ms_layered_grp_kernel(dc, nh, gg, &cfg.name);
-      if (cfg.kernel) cfg.nh = nh;
-    }
-    if (!cfg.kernel) cfg.kernel = qldpc::select_ms_layered_kernel(dc, g, &cfg.name);
+    // (several half-shots per wave, ms_layered_grp_kernel, measured 2x slower
+    // in round 2: at a fixed LDS budget it halves the waves per CU; removed)
+    cfg.kernel = qldpc::select_ms_layered_kernel(dc, g, &cfg.name);
     use_lblob = cfg.kernel != nullptr;
   }
   cfg.lblob = use_lblob;
@@ -640,21 +596,17 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
     // teams (the VGPR cap of 16 team waves) — LP118_2: 2 teams with all-LDS
     // tables, 3 with the row table alone global; the kernel is barrier /
     // latency-bound and BP-L p = 0.1 ran 175 -> 132 -> 108 ms per launch.
-    // QLDPC_BP_GT=0 (all LDS) / 1 (row table global) / 2 (default) override.
-    bool tgt = false;
+    // Schedules without the global image (n > 2048, a column degree > 31) run
+    // the all-LDS team kernel; QLDPC_BP_LG=0 forces it (tests).
     bool tlg = s->layered && !s->lgblob.empty();
-    if (const char* ev = getenv("QLDPC_BP_GT")) {
-      tgt = s->layered && !s->tblob.empty() && atoi(ev) == 1;
-      tlg = s->layered && !s->lgblob.empty() && atoi(ev) == 2;
-    }
-    if (tgt || tlg) team = 4;
+    if (const char* ev = getenv("QLDPC_BP_LG")) tlg = tlg && atoi(ev) != 0;
+    if (tlg) team = 4;
     if (const char* ev = getenv("QLDPC_BP_TEAM_W")) team = atoi(ev);
     if (tlg) {
       cfg.kernel = qldpc::select_bp_team_lg_kernel(dc, team, &cfg.name);
       cfg.tlg = cfg.kernel != nullptr;
     }
-    if (!cfg.kernel) cfg.kernel = qldpc::select_bp_team_kernel(s->layered, dc, team, tgt, &cfg.name);
-    cfg.tgt = tgt && !cfg.tlg && cfg.kernel != nullptr;
+    if (!cfg.kernel) cfg.kernel = qldpc::select_bp_team_kernel(s->layered, dc, team, &cfg.name);
     if (!cfg.kernel) team = 0;
   }
   cfg.team = team;
@@ -662,21 +614,18 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   int off_c2v, off_synw, off_parw, off_red;
   wave_layout(c, s->layered, algo, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw, use_lblob);
   if (team) team_layout(c, team, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw, &off_red);
-  if (cfg.nh > 1 || (use_lblob && cfg.name && strstr(cfg.name, "grp"))) {
-    grp_layout(c, &cfg.slice, &off_c2v, &off_synw);
-    cfg.wave_bytes = cfg.nh * cfg.slice;
-  }
   int max_lds = 0, dev = 0;
   HIP_TRY(hipGetDevice(&dev));
   HIP_TRY(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
   HIP_TRY(qldpc::configure_kernel(cfg.kernel, max_lds));
   const int blob = gtab ? QLDPC_FLOOD_HDR
-                        : cfg.tgt ? s->t_lds_bytes
                         : cfg.tlg ? s->lg_lds_bytes
                         : (int)(use_lblob ? s->lblob.size() : s->blob.size());
+  // BP kernels stage NumPy's libm tables behind every slice (DecodeArgs::off_libm)
+  const int libm = algo == QLDPC_ALGO_BP ? (int)sizeof(qldpc_libm_tab) : 0;
   int best_waves = 0;
   if (team) {  // one team (workgroup of `team` waves) per half-shot
-    const int lds = blob + cfg.wave_bytes;
+    const int lds = blob + cfg.wave_bytes + libm;
     int nb = 0;
     if (lds <= max_lds)
       HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cfg.kernel, 64 * team, (size_t)lds));
@@ -687,7 +636,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
     max_waves = 0;  // skip the wave-kernel search below
   }
   for (int w = max_waves; w >= 1; --w) {
-    const int lds = blob + w * cfg.wave_bytes;
+    const int lds = blob + w * cfg.wave_bytes + libm;
     if (lds > max_lds) continue;
     int nb = 0;
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cfg.kernel, 64 * w, (size_t)lds));
@@ -701,7 +650,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   // Tuning overrides (experiments only): QLDPC_WAVES_PER_WG, QLDPC_WG_PER_CU.
   if (const char* ev = team ? nullptr : getenv("QLDPC_WAVES_PER_WG")) {
     const int w = atoi(ev);
-    const int lds = blob + w * cfg.wave_bytes;
+    const int lds = blob + w * cfg.wave_bytes + libm;
     int nb = 0;
     if (w >= 1 && w <= max_waves && lds <= max_lds &&
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cfg.kernel, 64 * w, (size_t)lds) == hipSuccess && nb > 0) {
@@ -805,8 +754,6 @@ extern "C" int qldpc_decode_device_ex(const qldpc_code* code, const qldpc_schedu
   LaunchCfg* cfg = nullptr;
   int rc = launch_config(sched, algo, &cfg);
   if (rc) return rc;
-  if (ehat_format == QLDPC_FMT_BITS && cfg->slice)
-    return fail(QLDPC_EUNSUP, "bit-packed estimates are not written by ms_layered_grp_kernel (unset QLDPC_MS_GROUPS)");
 
   DecodeArgs a{};
   a.blob = sched->d_blob;
@@ -843,18 +790,6 @@ extern "C" int qldpc_decode_device_ex(const qldpc_code* code, const qldpc_schedu
     a.off_lay_rows = sched->lg_off_lrow;
     a.off_row_ptr = sched->lg_off_adj;
   }
-  if (cfg->tgt) {  // bp_team_kernel<.., true>: LDS part of tblob + its global row table
-    a.blob = sched->d_tblob;
-    a.blob_bytes = sched->t_lds_bytes;
-    a.off_cn_tab = sched->t_off_cn_tab;
-    a.off_vn_ptr = sched->t_off_vn_ptr;
-    a.off_lay_ptr = sched->t_off_lay_ptr;
-    a.off_lay_rows = sched->t_off_lay_rows;
-    a.off_adj_ptr = sched->t_off_adj_ptr;
-    a.off_adj_vars = sched->t_off_adj_vars;
-    a.off_row_ptr = a.off_chunk_dmax = a.off_vn_chk = 0;   // (not read by the team kernel)
-  }
-  if (cfg->slice) grp_layout(code, &a.wave_bytes, &a.off_c2v, &a.off_synw);   // per half-shot slice
   if (cfg->gtab) {  // global tables; the LDS holds wave state only
     a.blob = sched->d_fblob;
     a.blob_bytes = 0;
@@ -875,8 +810,11 @@ extern "C" int qldpc_decode_device_ex(const qldpc_code* code, const qldpc_schedu
   a.post = d_post;
   a.flags = d_flags;
   a.batch = batch;
-  // L_ch = np.log((1 - p) / max(p, eps))   (decoders.py:147, :232)
-  a.L = std::log((1.0 - p) / std::max(p, eps));
+  // L_ch = np.log((1 - p) / max(p, eps))   (decoders.py:147, :232), with
+  // NumPy's own log (SVML log8_ha, include/qldpc_libm.h): glibc's differs in
+  // the last bit for ~0.2 % of priors
+  a.L = qldpc_prior_llr(p, eps);
+  a.off_libm = algo == QLDPC_ALGO_BP ? cfg->lds - (int)sizeof(qldpc_libm_tab) : 0;
   a.L32 = (float)a.L;
   a.beta = beta;
   a.eps = eps;
@@ -900,7 +838,7 @@ extern "C" int qldpc_decode_device_ex(const qldpc_code* code, const qldpc_schedu
   }
   int cus = 0;
   HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  const int64_t per_block = cfg->team ? 1 : (int64_t)cfg->waves * cfg->nh;
+  const int64_t per_block = cfg->team ? 1 : (int64_t)cfg->waves;
   const int64_t need = (batch + per_block - 1) / per_block;
   const int64_t resident = (int64_t)cfg->blocks_per_cu * cus;
   const int grid = (int)std::max<int64_t>(1, std::min(need, resident));

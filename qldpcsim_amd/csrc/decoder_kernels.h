@@ -48,6 +48,7 @@ struct DecodeArgs {
   // (bit j % 64 of word j / 64) instead of one byte per bit
   int syn_bits, eh_bits;
   int wm, wn;                 // ceil(m / 64), ceil(n / 64)
+  int off_libm;               // BP: LDS byte offset of the qldpc_libm_tab image (after every slice)
 };
 
 // `name` (nullable) receives the kernel's name as rocprofv3 reports it
@@ -59,11 +60,8 @@ int ms_flood_max_waves(int kc);                      // waves per workgroup it w
 const void* select_ms_layered_kernel(int dc, int g, const char** name);
 // layered BP teams, every graph table in global memory (gblob of the schedule)
 const void* select_bp_team_lg_kernel(int dc, int w, const char** name);
-// layered MS, NH half-shots per wave (64 / NH lanes each), G lanes per check
-const void* select_ms_layered_grp_kernel(int dc, int nh, int g, const char** name);
 // BP, uniform row degree 7/8: one team of W waves per half-shot, edge-parallel check nodes
-// gt: the row table in global memory, LDS image = the team blob (tblob)
-const void* select_bp_team_kernel(bool layered, int dc, int w, bool gt, const char** name);
+const void* select_bp_team_kernel(bool layered, int dc, int w, const char** name);
 hipError_t launch_decode(const void* kernel, const DecodeArgs& args, int grid, int block,
                          int lds_bytes, hipStream_t stream);
 hipError_t configure_kernel(const void* kernel, int lds_bytes);

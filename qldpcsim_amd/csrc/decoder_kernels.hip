@@ -44,6 +44,18 @@
 
 namespace qldpc {
 
+// NumPy's tanh / SVML's atanh tables (include/qldpc_libm.h). BP kernels copy
+// this image into LDS (DecodeArgs::off_libm) once per workgroup: the lookups
+// are per lane (data-dependent intervals), 10-13 per edge and iteration.
+__constant__ qldpc_libm_tab qldpc_libm_dev = QLDPC_LIBM_TAB_INIT;
+
+__device__ __forceinline__ const qldpc_libm_tab* stage_libm(unsigned char* lds, int off) {
+  const uint4* src = (const uint4*)&qldpc_libm_dev;
+  uint4* dst = (uint4*)(lds + off);
+  for (int i = threadIdx.x; i < (int)(sizeof(qldpc_libm_tab) / 16); i += blockDim.x) dst[i] = src[i];
+  return (const qldpc_libm_tab*)(lds + off);
+}
+
 __device__ __forceinline__ void wave_sync() {
   // Lanes of one wave exchange data through LDS between phases. DS
   // instructions of a wave complete in order; the fences only stop the
@@ -241,6 +253,7 @@ struct LdsView {
   const uint16_t* lay_rows; // [*]
   const uint16_t* adj_ptr;  // [L+1]
   const uint16_t* adj_vars; // [*]
+  const qldpc_libm_tab* lt; // BP: NumPy libm tables (LDS)
 };
 
 // Graph table entry formats (capi.cpp builds them):
@@ -532,7 +545,7 @@ __device__ __forceinline__ uint32_t cn_update(const DecodeArgs& a, const LdsView
       const double pj = post[j];
       par ^= (uint32_t)(pj < 0.0);
       const double v = pj - c2v[pos];                // v2c (:269)
-      const double th = qldpc_tanh(v / 2.0);         // (:254) reproducible tanh
+      const double th = qldpc_tanh_t(v / 2.0, g.lt->tanh_c);   // (:254) np.tanh
       prod *= th;                                    // np.prod: sequential fold
       c2v[pos] = th;                                 // scratch: own edge, rewritten below
     }
@@ -543,7 +556,7 @@ __device__ __forceinline__ uint32_t cn_update(const DecodeArgs& a, const LdsView
         const int j = tab_var<DC>(t), pos = tab_pos<DC>(t);
         const double pj = post[j];
         par ^= (uint32_t)(pj < 0.0);
-        const double th = qldpc_tanh((pj - c2v[pos]) / 2.0);
+        const double th = qldpc_tanh_t((pj - c2v[pos]) / 2.0, g.lt->tanh_c);
         prod *= th;
         c2v[pos] = th;
       }
@@ -556,7 +569,7 @@ __device__ __forceinline__ uint32_t cn_update(const DecodeArgs& a, const LdsView
       double th2 = prod / th;                        // (:256)
       if (__builtin_fabs(th2) >= lim)                // (:257-258)
         th2 = th2 - a.eps * (th2 > 0.0 ? 1.0 : (th2 < 0.0 ? -1.0 : 0.0));
-      double val = 2.0 * qldpc_atanh(th2);           // (:259) reproducible atanh
+      double val = 2.0 * qldpc_atanh_t(th2, g.lt->atanh_hl, g.lt->atanh_rcp);   // (:259) np.arctanh
       if (synb) val = -val;                          // (:260-261)
       if (!__builtin_isfinite(val)) fl |= FLAG_NONFINITE;
       c2v[pos] = val;
@@ -659,6 +672,11 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) decode_kernel(DecodeArgs a)
   g.lay_rows = (const uint16_t*)(lds + a.off_lay_rows);
   g.adj_ptr = (const uint16_t*)(lds + a.off_adj_ptr);
   g.adj_vars = (const uint16_t*)(lds + a.off_adj_vars);
+  g.lt = nullptr;
+  if constexpr (ALGO == ALGO_BP) {
+    g.lt = stage_libm(lds, a.off_libm);
+    __syncthreads();
+  }
 
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -1419,285 +1437,6 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
 }
 
 // ---------------------------------------------------------------------------
-// Layered / serial min-sum with NH half-shots per wavefront (LPH = 64 / NH
-// lanes each). Layers are short (LP118_0: 16 / 32 rows, 128-208 adjacent
-// variables), so with one half-shot per wave most lanes idle in the check
-// node and every per-layer fixed cost (stop test, loop control, barriers) is
-// paid per half-shot. Here each lane group runs its own half-shot, iteration
-// and layer: a group that converges (or reaches max_iter) writes its outputs
-// and starts its next half-shot while the others carry on, so early-stopping
-// decodes waste no lanes. Same arithmetic as ms_layered_kernel, bit for bit:
-// CN over the layer's rows with G lanes per check (cn_ms_split), VN over the
-// layer's adjacent variables, filtered stop test with the exact check behind
-// it. Loops run to the largest bound among the groups, with per-lane masks.
-// ---------------------------------------------------------------------------
-template <int LPH>
-__device__ __forceinline__ uint32_t group_xor(uint32_t x, int grp) {
-  x ^= dpp_u32<kDppQuadXor1>(x);
-  x ^= dpp_u32<kDppQuadXor2>(x);
-  x ^= dpp_u32<kDppHalfMirror>(x);
-  x ^= dpp_u32<kDppRowMirror>(x);
-  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 0), r1 = (uint32_t)__builtin_amdgcn_readlane((int)x, 16);
-  const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)x, 32), r3 = (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
-  if constexpr (LPH == 16) {
-    return grp == 0 ? r0 : grp == 1 ? r1 : grp == 2 ? r2 : r3;
-  } else if constexpr (LPH == 32) {
-    return grp == 0 ? (r0 ^ r1) : (r2 ^ r3);
-  } else {
-    return r0 ^ r1 ^ r2 ^ r3;
-  }
-}
-
-// wave-wide maximum of a group-uniform non-negative value
-template <int LPH>
-__device__ __forceinline__ int groups_max(int x) {
-  int r = __builtin_amdgcn_readlane(x, 0);
-#pragma unroll
-  for (int g = 1; g < 64 / LPH; ++g) r = max(r, __builtin_amdgcn_readlane(x, g * LPH));
-  return r;
-}
-
-template <int LPH>
-__device__ __forceinline__ uint64_t group_mask(int grp) {
-  return LPH == 64 ? ~0ull : (((1ull << (LPH & 63)) - 1ull) << (LPH * grp));
-}
-
-// Per-group half-shot queue (HalfShotQueue's guided chunks, claimed by the
-// group's first lane and broadcast to the group).
-struct GroupQueue {
-  long long hs, end, stride, batch;
-  uint32_t* q;
-  uint32_t tk, tlen, seen;
-  __device__ __forceinline__ GroupQueue(const DecodeArgs& a, long long slot, long long stride_)
-      : hs(slot), end(slot + 1), stride(stride_), batch(a.batch), q(a.queue), tk(0), tlen(1), seen(0) {}
-  __device__ __forceinline__ void prefetch(int sl) {
-    if (q && hs + 1 == end) {
-      const long long rem = batch - stride - (long long)seen;
-      long long len = rem / (4 * stride);
-      len = len < 1 ? 1 : (len > 64 ? 64 : len);
-      tlen = (uint32_t)len;
-      if (sl == 0) tk = atomicAdd(q, tlen);
-    }
-  }
-  __device__ __forceinline__ void advance(int leader) {
-    if (!q) {
-      hs += stride;
-      return;
-    }
-    hs += 1;
-    if (hs < end) return;
-    const uint32_t t = (uint32_t)__shfl((int)tk, leader, 64);
-    seen = t + tlen;
-    hs = stride + (long long)t;
-    end = hs + tlen;
-  }
-};
-
-template <int K, int LPH>
-__device__ __forceinline__ uint32_t vn_layer_grp(const uint32_t* adj_info, const uint32_t* avar, float* colS,
-                                                 const float* c2v, int v0, int nadj, int pa, int sl, float thr) {
-  uint32_t acc = 0;
-  for (int cb = 0; cb < pa; cb += 2 * LPH) {
-    uint32_t info[2];
-    bool in[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int i = cb + h * LPH + sl;
-      in[h] = i < nadj;
-      info[h] = adj_info[v0 + (in[h] ? i : 0)];
-    }
-    float old[2];
-    uint32_t av[2];
-    float x[2][K];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      old[h] = colS[info[h] >> 21];
-      av[h] = avar[info[h] >> 21];
-      const float* c = c2v + (info[h] & 0xffffu);
-#pragma unroll
-      for (int t = 0; t < K; ++t) x[h][t] = c[t];
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int d = (int)((info[h] >> 16) & 31u);
-      float s = 0.0f;                                       // sequential, ascending check (:172)
-#pragma unroll
-      for (int t = 0; t < K; ++t) s += (t < d) ? x[h][t] : 0.0f;
-      if (in[h]) colS[info[h] >> 21] = s;
-      const bool flip = in[h] && ((old[h] < thr) != (s < thr));
-      acc ^= flip ? av[h] : 0u;
-    }
-  }
-  return acc;
-}
-
-template <int DC, int NH, int G>
-__global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_grp_kernel(DecodeArgs a) {
-  constexpr int LPH = 64 / NH;
-  constexpr int CPP = LPH / G;                                  // checks per CN pass per group
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  {
-    const uint4* src = (const uint4*)a.blob;
-    uint4* dst = (uint4*)lds;
-    const int nvec = a.blob_bytes >> 4;
-    for (int i = threadIdx.x; i < nvec; i += blockDim.x) dst[i] = src[i];
-  }
-  __syncthreads();
-  const uint32_t* ltab = (const uint32_t*)(lds + a.off_cn_tab);      // [Q][8]
-  const uint16_t* lrow = (const uint16_t*)(lds + a.off_lay_rows);    // [Q]
-  const uint16_t* lay_ptr = (const uint16_t*)(lds + a.off_lay_ptr);  // [L+1]
-  const uint16_t* adj_ptr = (const uint16_t*)(lds + a.off_adj_ptr);  // [L+1]
-  const uint32_t* adj_info = (const uint32_t*)(lds + a.off_row_ptr); // [A] var<<21 | deg<<16 | csc start
-  const uint8_t* adj_dmax = (const uint8_t*)(lds + a.off_chunk_dmax);// [L]
-  const uint32_t* avar = (const uint32_t*)(lds + a.off_vn_chk);      // [n] filter words
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  const int waves = blockDim.x >> 6;
-  const int grp = lane / LPH, sl = lane % LPH, leader = grp * LPH;
-  const uint64_t gmask = group_mask<LPH>(grp);
-  // this group's half-shot slice: colS f32[n] | c2v f32[E + 8] | syndrome u8[m]
-  unsigned char* ws = lds + a.blob_bytes + (wid * NH + grp) * a.wave_bytes;
-  float* colS = (float*)ws;
-  unsigned char* c2v_b = ws + a.off_c2v;
-  float* c2v = (float*)c2v_b;
-  uint8_t* synb = ws + a.off_synw;
-  const uint32_t post_b = lds_addr(colS), c2v_a = lds_addr(c2v_b);
-  const int m = a.m, n = a.n, nl = a.n_layers;
-  const float thr = a.hd_thresh;
-  const double L = a.L;
-
-  GroupQueue Q(a, ((long long)blockIdx.x * waves + wid) * NH + grp, (long long)gridDim.x * waves * NH);
-  bool active = false;
-  int lay = 0, it = 0, fl = 0;
-  bool first = true;
-  uint32_t F = 0, B = 0;
-
-  // starts half-shot Q.hs in this group's slice (lanes of starting groups only)
-  auto start = [&]() {
-    for (int c = sl; c < m; c += LPH) synb[c] = (uint8_t)syn_bit(a, Q.hs, c);
-    for (int j = sl; j < n; j += LPH) colS[j] = 0.0f;            // post = L, c2v = 0 (:148-150)
-    for (int p = sl; p < a.E; p += LPH) c2v[p] = 0.0f;
-    lay = 0;
-    it = 0;
-    fl = 0;
-    first = true;
-    F = (L < 0.0) ? a.filt_all : 0u;
-  };
-
-  active = Q.hs < a.batch;
-  if (active) {
-    Q.prefetch(sl);
-    start();
-  }
-  wave_sync();
-  {
-    uint32_t b = 0;
-    if (active)
-      for (int c = sl; c < m; c += LPH) b ^= synb[c] ? a.wc[c] : 0u;
-    B = group_xor<LPH>(b, grp);
-  }
-
-  while (ballot(active) != 0) {
-    // ---- check nodes of each group's current layer (Jacobi, :155-169)
-    const int q0 = lay_ptr[lay], q1 = lay_ptr[lay + 1];
-    const int rows = active ? q1 - q0 : 0;
-    const int prow = groups_max<LPH>(rows);
-    for (int qb = 0; qb < prow; qb += CPP) {
-      const int qi = qb + sl / G;
-      const bool live = qi < rows;
-      const int qs = q0 + (live ? qi : 0);
-      const int c = lrow[qs];
-      cn_ms_split<DC, G>(a, ltab + qs * 8, sl & (G - 1), live, (uint32_t)synb[c], first, post_b, c2v_a, fl);
-    }
-    first = false;
-    wave_sync();
-    // ---- variable nodes adjacent to the layer (:172-174)
-    const int v0 = adj_ptr[lay], v1 = adj_ptr[lay + 1];
-    const int nadj = active ? v1 - v0 : 0;
-    const int pa = groups_max<LPH>(nadj);
-    const int kmax = groups_max<LPH>(active ? ((int)adj_dmax[lay] & 31) : 0);
-    uint32_t acc = 0;
-    switch (kmax) {
-      case 3: acc = vn_layer_grp<3, LPH>(adj_info, avar, colS, c2v, v0, nadj, pa, sl, thr); break;
-      case 4: acc = vn_layer_grp<4, LPH>(adj_info, avar, colS, c2v, v0, nadj, pa, sl, thr); break;
-      case 5: acc = vn_layer_grp<5, LPH>(adj_info, avar, colS, c2v, v0, nadj, pa, sl, thr); break;
-      case 6: acc = vn_layer_grp<6, LPH>(adj_info, avar, colS, c2v, v0, nadj, pa, sl, thr); break;
-      default:
-        for (int i = sl; i < pa; i += LPH) {
-          if (i < nadj) {
-            const uint32_t info = adj_info[v0 + i];
-            const int j = (int)(info >> 21), d = (int)((info >> 16) & 31u);
-            const float old = colS[j];
-            const float s = ms_colsum_sw(c2v + (info & 0xffffu), d, kmax);
-            colS[j] = s;
-            if ((old < thr) != (s < thr)) acc ^= avar[j];
-          }
-        }
-    }
-    F ^= group_xor<LPH>(acc, grp);
-    wave_sync();
-    // ---- stop test (:175-176): filters, then the exact test for groups that pass
-    const bool cand = active && F == B;
-    bool conv = false;
-    if (ballot(cand) != 0) {
-      uint32_t un = 0;
-      if (cand) {
-        for (int c = sl; c < m; c += LPH) {
-          const uint4 t0 = *(const uint4*)(a.rtab + 8 * (size_t)c);
-          const uint4 t1 = *(const uint4*)(a.rtab + 8 * (size_t)c + 4);
-          const uint32_t t[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
-          uint32_t par = 0;
-#pragma unroll
-          for (int k = 0; k < DC; ++k) par ^= (uint32_t)(colS[t[k]] < thr);
-          un |= par ^ (uint32_t)synb[c];
-        }
-      }
-      conv = cand && (ballot(un != 0) & gmask) == 0;
-    }
-    const bool done = active && (conv || (lay + 1 == nl && it + 1 == a.max_iter));
-    if (active && !done) {
-      if (++lay == nl) {
-        lay = 0;
-        ++it;
-      }
-    }
-    if (ballot(done) != 0) {
-      const bool fmz = (ballot((fl & FLAG_MIN_ZERO) != 0) & gmask) != 0;
-      if (done) {
-        // ê and posteriors in original column order
-        const long long hs = Q.hs;
-        double* po = a.post ? a.post + hs * (long long)n : nullptr;
-        for (int jo = sl; jo < n; jo += LPH) {
-          const double pv = L + (double)colS[a.vinv[jo]];
-          put_ehat(a, hs, jo, pv < 0.0);
-          if (po) po[jo] = pv;
-        }
-        if (sl == 0) {
-          a.iters[hs] = conv ? it + 1 : a.max_iter;
-          if (a.flags) a.flags[hs] = (int32_t)((fmz ? FLAG_MIN_ZERO : 0) | (conv ? FLAG_CONVERGED : 0));
-        }
-        Q.advance(leader);
-        active = Q.hs < a.batch;
-      }
-      wave_sync();                                               // slice reuse
-      const bool restart = done && active;
-      if (restart) {
-        Q.prefetch(sl);
-        start();
-      }
-      wave_sync();
-      if (ballot(restart) != 0) {
-        uint32_t b = 0;
-        if (restart)
-          for (int c = sl; c < m; c += LPH) b ^= synb[c] ? a.wc[c] : 0u;
-        const uint32_t nb = group_xor<LPH>(b, grp);
-        if (restart) B = nb;
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Sum-product BP for uniform row degree DC (7 or 8): one TEAM of W wavefronts
 // (one workgroup) decodes one half-shot, with the check-node update spread
 // over the edges — 8 lanes per check, lane k owns edge k — instead of a lane
@@ -1718,13 +1457,14 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_grp_kernel(Decod
 // ---------------------------------------------------------------------------
 // edge k of a check whose table word t (row table entry 8c + k) is given
 template <int DC>
-__device__ __forceinline__ uint32_t cn_bp_word(const DecodeArgs& a, uint32_t t, bool valid, int k, int lane,
-                                               uint32_t synb, const double* post, double* c2v, int& fl) {
+__device__ __forceinline__ uint32_t cn_bp_word(const DecodeArgs& a, const qldpc_libm_tab* lt, uint32_t t, bool valid,
+                                               int k, int lane, uint32_t synb, const double* post, double* c2v,
+                                               int& fl) {
   const bool ek = valid && k < DC;
   const int j = (int)((t & 0xffffu) >> 3), p = (int)(t >> 18);
   const double pj = ek ? post[j] : 0.0;
   double th = 1.0;
-  if (ek) th = qldpc_tanh((pj - c2v[p]) / 2.0);           // v2c (:269), tanh (:254)
+  if (ek) th = qldpc_tanh_t((pj - c2v[p]) / 2.0, lt->tanh_c);   // v2c (:269), np.tanh (:254)
   // np.prod: sequential left fold over the check's edges in ascending variable
   // order, ((t_0 t_1) t_2) ..., formed redundantly by every lane of the group
   // from the group's t values (one permute each): same rounding as a
@@ -1739,18 +1479,19 @@ __device__ __forceinline__ uint32_t cn_bp_word(const DecodeArgs& a, uint32_t t, 
   const uint32_t par = (uint32_t)__builtin_popcount((uint32_t)(hb >> (lane & 56)) & 0xffu) & 1u;
   if (ek) {
     if (th == 0.0) fl |= FLAG_NONFINITE;
-    // P / th (:256). QLDPC_DIV is IEEE division for operands in the normal
-    // range (|th| <= 1 and |P| <= |th| here); a wave holding a zero, tiny or
+    // P / th (:256). QLDPC_DIV is IEEE division for nonzero operands in the
+    // normal range (|th| <= 1 and |P| <= |th| here); a wave holding a zero
+    // (a -0 product keeps its sign only through v_div_fixup), tiny or
     // non-finite one divides the general way.
     double th2;
-    if (__builtin_expect(ballot(!(__builtin_fabs(th) > 1e-150 && (P == 0.0 || __builtin_fabs(P) > 1e-150))) != 0, 0))
+    if (__builtin_expect(ballot(!(__builtin_fabs(th) > 1e-150 && __builtin_fabs(P) > 1e-150)) != 0, 0))
       th2 = P / th;
     else
       th2 = QLDPC_DIV(P, th);
     // (:257-258): |th2| >= 1 - eps implies th2 != 0, so eps * sign(th2) is
     // copysign(eps, th2) (a NaN compares false and stays)
     th2 = (__builtin_fabs(th2) >= 1.0 - a.eps) ? th2 - __builtin_copysign(a.eps, th2) : th2;
-    double val = 2.0 * qldpc_atanh(th2);                  // (:259)
+    double val = 2.0 * qldpc_atanh_t(th2, lt->atanh_hl, lt->atanh_rcp);   // (:259) np.arctanh
     if (synb) val = -val;                                 // (:260-261)
     if (!__builtin_isfinite(val)) fl |= FLAG_NONFINITE;
     c2v[p] = val;
@@ -1763,14 +1504,13 @@ __device__ __forceinline__ uint32_t cn_bp_group(const DecodeArgs& a, const LdsVi
                                                 int k, int lane, uint32_t synb, const double* post,
                                                 double* c2v, int& fl) {
   const uint32_t t = (valid && k < DC) ? g.cn_tab[8 * c + k] : 0u;
-  return cn_bp_word<DC>(a, t, valid, k, lane, synb, post, c2v, fl);
+  return cn_bp_word<DC>(a, g.lt, t, valid, k, lane, synb, post, c2v, fl);
 }
 
-// GT: the check-row table (8 words per check) is read from global memory
-// (L1/L2-resident) and the LDS image holds only the variable / layer tables
-// (tblob, capi.cpp): LP118_2's 34 KB image shrinks to 12 KB, so a CU holds 3
-// teams' float64 state instead of 2.
-template <bool LAYERED, int DC, int W, bool GT = false>
+// Every graph table in LDS: the flooding BP kernel (VALU-bound), and the
+// layered fallback when the schedule has no global layer image (n > 2048 or a
+// column degree > 31, capi.cpp); bp_team_lg_kernel is the layered default.
+template <bool LAYERED, int DC, int W>
 __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) bp_team_kernel(DecodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   {
@@ -1779,9 +1519,10 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
     const int nvec = a.blob_bytes >> 4;
     for (int i = threadIdx.x; i < nvec; i += blockDim.x) dst[i] = src[i];
   }
-  __syncthreads();
   LdsView g;
-  g.cn_tab = GT ? (const uint32_t*)(a.blob + a.off_cn_tab) : (const uint32_t*)(lds + a.off_cn_tab);
+  g.lt = stage_libm(lds, a.off_libm);
+  __syncthreads();
+  g.cn_tab = (const uint32_t*)(lds + a.off_cn_tab);
   g.row_ptr = (const uint16_t*)(lds + a.off_row_ptr);
   g.vn_info = (const uint32_t*)(lds + a.off_vn_ptr);
   g.chunk_dmax = (const uint8_t*)(lds + a.off_chunk_dmax);
@@ -1983,6 +1724,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
     const int nvec = a.blob_bytes >> 4;
     for (int i = threadIdx.x; i < nvec; i += blockDim.x) dst[i] = src[i];
   }
+  const qldpc_libm_tab* lt = stage_libm(lds, a.off_libm);
   __syncthreads();
   const uint32_t* ltab_g = (const uint32_t*)(a.blob + a.off_cn_tab);      // [Q][8] rows, layer order
   const uint16_t* lrow_g = (const uint16_t*)(a.blob + a.off_lay_rows);    // [Q]    their checks
@@ -2075,7 +1817,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
             const bool valid = q0 + GP * i + grp < q1;
             const int c = (int)pc[i];
             const uint32_t sb = valid ? (synw[c >> 5] >> (c & 31)) & 1u : 0u;
-            (void)cn_bp_word<DC>(a, pt[i], valid, k, lane, sb, post, c2v, fl);
+            (void)cn_bp_word<DC>(a, lt, pt[i], valid, k, lane, sb, post, c2v, fl);
           }
         }
         for (int qb = q0 + GP * NPF; qb < q1; qb += GP) {  // layers of more than NPF passes
@@ -2084,7 +1826,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
           const int c = valid ? (int)lrow_g[q] : 0;
           const uint32_t t = (valid && k < DC) ? ltab_g[8 * q + k] : 0u;
           const uint32_t sb = valid ? (synw[c >> 5] >> (c & 31)) & 1u : 0u;
-          (void)cn_bp_word<DC>(a, t, valid, k, lane, sb, post, c2v, fl);
+          (void)cn_bp_word<DC>(a, lt, t, valid, k, lane, sb, post, c2v, fl);
         }
         rows_pf(l + 1 < nl ? l + 1 : 0);                  // in flight during the VN
         __syncthreads();
@@ -2176,17 +1918,12 @@ const void* select_ms_flood_kernel(int dc, int kc, const char** name) {
   return nullptr;
 }
 
-const void* select_bp_team_kernel(bool layered, int dc, int w, bool gt, const char** name) {
+const void* select_bp_team_kernel(bool layered, int dc, int w, const char** name) {
 #define QLDPC_BPT(L, D, Wn) \
-  if (!gt && layered == L && dc == D && w == Wn) QLDPC_NAMED((&bp_team_kernel<L, D, Wn>), "bp_team_kernel<" #L ", " #D ", " #Wn ", false>");
+  if (layered == L && dc == D && w == Wn) QLDPC_NAMED((&bp_team_kernel<L, D, Wn>), "bp_team_kernel<" #L ", " #D ", " #Wn ">");
   QLDPC_BPT(false, 7, 4) QLDPC_BPT(false, 8, 4) QLDPC_BPT(true, 7, 4) QLDPC_BPT(true, 8, 4)
   QLDPC_BPT(false, 7, 8) QLDPC_BPT(false, 8, 8) QLDPC_BPT(true, 7, 8) QLDPC_BPT(true, 8, 8)
 #undef QLDPC_BPT
-#define QLDPC_BPG(L, D, Wn)                                  \
-  if (gt && layered == L && dc == D && w == Wn)              \
-    QLDPC_NAMED((&bp_team_kernel<L, D, Wn, true>), "bp_team_kernel<" #L ", " #D ", " #Wn ", true>");
-  QLDPC_BPG(true, 7, 4) QLDPC_BPG(true, 8, 4) QLDPC_BPG(true, 7, 8) QLDPC_BPG(true, 8, 8)
-#undef QLDPC_BPG
   return nullptr;
 }
 
@@ -2203,17 +1940,6 @@ const void* select_ms_layered_kernel(int dc, int g, const char** name) {
   QLDPC_MSL(7, 0) QLDPC_MSL(8, 0) QLDPC_MSL(7, 1) QLDPC_MSL(8, 1) QLDPC_MSL(7, 2) QLDPC_MSL(8, 2)
   QLDPC_MSL(7, 4) QLDPC_MSL(8, 4) QLDPC_MSL(7, 8) QLDPC_MSL(8, 8)
 #undef QLDPC_MSL
-  return nullptr;
-}
-
-const void* select_ms_layered_grp_kernel(int dc, int nh, int g, const char** name) {
-#define QLDPC_MSG(D, N, Gn)            \
-  if (dc == D && nh == N && g == Gn) \
-    QLDPC_NAMED((&ms_layered_grp_kernel<D, N, Gn>), "ms_layered_grp_kernel<" #D ", " #N ", " #Gn ">");
-  QLDPC_MSG(7, 2, 1) QLDPC_MSG(8, 2, 1) QLDPC_MSG(7, 2, 2) QLDPC_MSG(8, 2, 2)
-  QLDPC_MSG(7, 4, 1) QLDPC_MSG(8, 4, 1) QLDPC_MSG(7, 4, 2) QLDPC_MSG(8, 4, 2)
-  QLDPC_MSG(7, 1, 1) QLDPC_MSG(8, 1, 1) QLDPC_MSG(7, 1, 4) QLDPC_MSG(8, 1, 4)
-#undef QLDPC_MSG
   return nullptr;
 }
 

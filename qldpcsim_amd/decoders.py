@@ -273,6 +273,24 @@ def _device_order_min():
     return int(os.environ.get("QLDPC_OSD_DEVICE_MIN", "4096"))
 
 
+def _on_stream(stream):
+    """Context that makes `stream` (a raw HIP stream handle, or None = torch's
+    current stream) the current stream, so every kernel, copy and event of
+    one OSD stage is ordered on it."""
+    import contextlib
+    import torch
+    if stream is None:
+        return contextlib.nullcontext()
+    return torch.cuda.stream(torch.cuda.ExternalStream(stream))
+
+
+def release_workspaces():
+    """Free the grow-only device OSD spill workspaces and pinned staging
+    buffers (they are reused across batches while a sweep runs)."""
+    _DEVBUF.clear()
+    _PINNED.clear()
+
+
 def osd_device_stage(items, stream=None, slot0=0, order=0):
     """First half of the device OSD: find each decode's non-converged shots
     (one device sync), then queue asynchronously on the device: the
@@ -282,52 +300,66 @@ def osd_device_stage(items, stream=None, slot0=0, order=0):
     by osd_device_finish. `slot0` selects the pinned buffer set (pipelined
     callers alternate). QLDPC_OSD_HOST_ORDER=1 (A/B only) or n > 2048 sends
     every shot through NumPy's order, as osd_perms computes it."""
-    import torch
     staged = []
-    for slot, (H, syn, res) in enumerate(items):
-        if res.post is None:
-            raise ValueError("apply_osd_device needs the decode's posteriors (want_post=True)")
-        dev = res.ehat.device
-        bad = ((res.flags & _lib.FLAG_CONVERGED) == 0).nonzero().flatten()
-        k = int(bad.numel())
-        if k == 0:
-            staged.append(None)
-            continue
-        n = res.post.shape[1]
-        code = _lib.code_for(H, dev.index)
-        post_b = res.post.index_select(0, bad)
-        syn_b = syn.index_select(0, bad)
-        e_b = res.ehat.index_select(0, bad)
-        status = torch.empty(k, dtype=torch.int32, device=dev)
-        cs = torch.cuda.current_stream(dev)
-        st = stream if stream is not None else cs.cuda_stream
-        status_h = _pinned(("status", slot0 + slot), (k,), torch.int32)
-        on_dev = n <= 2048 and k >= _device_order_min() and not _host_order_only()
-        spill = None
-        if on_dev:
-            perm = torch.empty((k, n), dtype=torch.int32, device=dev)
-            tie = torch.empty(k, dtype=torch.int32, device=dev)
-            # the shots left to NumPy's order copy their posteriors into a
-            # spill buffer (one DMA copy for the host later, no gather kernel)
-            cap = k // 2 + 1024
-            sp_post = _device_buf(("spill_post", slot0 + slot), (cap, n), torch.float64, dev)
-            sp_idx = _device_buf(("spill_idx", slot0 + slot), (cap,), torch.int32, dev)
-            sp_cnt = _device_buf(("spill_cnt", slot0 + slot), (1,), torch.int32, dev)
-            sp_cnt.zero_()
-            _lib.check(_lib.lib.qldpc_osd_device_ordered_ex(
-                code.handle, k, syn_b.data_ptr(), post_b.data_ptr(), int(order), e_b.data_ptr(),
-                status.data_ptr(), perm.data_ptr(), tie.data_ptr(), sp_post.data_ptr(), sp_idx.data_ptr(),
-                sp_cnt.data_ptr(), cap, st))
-            cnt_h = _pinned(("spill_cnt", slot0 + slot), (1,), torch.int32)
-            cnt_h.copy_(sp_cnt, non_blocking=True)
-            spill = (sp_post, sp_idx, cnt_h, cap)
-        else:
-            status.fill_(2)                            # every shot takes NumPy's order
-        status_h.copy_(status, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(cs)
-        staged.append((bad, post_b, syn_b, e_b, status, status_h, ev, slot0 + slot, on_dev, spill))
+    with _on_stream(stream):
+        for slot, (H, syn, res) in enumerate(items):
+            staged.append(_osd_stage_one(H, syn, res, slot0 + slot, order))
     return staged
+
+
+def _osd_stage_one(H, syn, res, slot, order):
+    import torch
+    if res.post is None:
+        raise ValueError("apply_osd_device needs the decode's posteriors (want_post=True)")
+    m, n = np.shape(H)
+    B = res.post.shape[0]
+    # the OSD kernels read one byte per check / variable: bit-packed decodes
+    # (ehat_bits, int64 word syndromes) must be unpacked first
+    if not (syn.dtype == torch.uint8 and tuple(syn.shape) == (B, m)):
+        raise ValueError(f"OSD needs uint8 [B, {m}] syndromes (unpack_bits a word batch first)")
+    if not (res.ehat.dtype == torch.uint8 and tuple(res.ehat.shape) == (B, n)):
+        raise ValueError(f"OSD needs uint8 [B, {n}] estimates (decode without ehat_bits)")
+    dev = res.ehat.device
+    bad = ((res.flags & _lib.FLAG_CONVERGED) == 0).nonzero().flatten()
+    k = int(bad.numel())
+    if k == 0:
+        return None
+    n = res.post.shape[1]
+    code = _lib.code_for(H, dev.index)
+    post_b = res.post.index_select(0, bad)
+    syn_b = syn.index_select(0, bad)
+    e_b = res.ehat.index_select(0, bad)
+    status = torch.empty(k, dtype=torch.int32, device=dev)
+    cs = torch.cuda.current_stream(dev)
+    st = cs.cuda_stream
+    status_h = _pinned(("status", slot), (k,), torch.int32)
+    on_dev = n <= 2048 and k >= _device_order_min() and not _host_order_only()
+    spill = None
+    if on_dev:
+        perm = torch.empty((k, n), dtype=torch.int32, device=dev)
+        tie = torch.empty(k, dtype=torch.int32, device=dev)
+        # the shots left to NumPy's order copy their posteriors into a
+        # spill buffer (one DMA copy for the host later, no gather kernel);
+        # at most 256 MiB per buffer — a batch that spills more takes the
+        # gather path in osd_device_finish
+        cap = min(k // 2 + 1024, max(1024, (256 << 20) // (8 * n)))
+        sp_post = _device_buf(("spill_post", slot), (cap, n), torch.float64, dev)
+        sp_idx = _device_buf(("spill_idx", slot), (cap,), torch.int32, dev)
+        sp_cnt = _device_buf(("spill_cnt", slot), (1,), torch.int32, dev)
+        sp_cnt.zero_()
+        _lib.check(_lib.lib.qldpc_osd_device_ordered_ex(
+            code.handle, k, syn_b.data_ptr(), post_b.data_ptr(), int(order), e_b.data_ptr(),
+            status.data_ptr(), perm.data_ptr(), tie.data_ptr(), sp_post.data_ptr(), sp_idx.data_ptr(),
+            sp_cnt.data_ptr(), cap, st))
+        cnt_h = _pinned(("spill_cnt", slot), (1,), torch.int32)
+        cnt_h.copy_(sp_cnt, non_blocking=True)
+        spill = (sp_post, sp_idx, cnt_h, cap)
+    else:
+        status.fill_(2)                            # every shot takes NumPy's order
+    status_h.copy_(status, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(cs)
+    return (bad, post_b, syn_b, e_b, status, status_h, ev, slot, on_dev, spill)
 
 
 def osd_staged_on_device(staged):
@@ -357,54 +389,58 @@ def osd_device_finish(items, staged, order, stream=None):
     the GPU elimination; then the corrected estimates are scattered back, all
     queued asynchronously. res.osd_status keeps 0 / 1 per shot (1: the
     reference's IndexError case, raised by osd_status_check)."""
-    import torch
-    for (H, syn, res), sg in zip(items, staged):
-        if sg is None:
-            continue
-        bad, post_b, syn_b, e_b, status, status_h, ev, slot, _, spill = sg
-        dev = res.ehat.device
-        code = _lib.code_for(H, dev.index)
-        ev.synchronize()
-        redo = (status_h.numpy() == 2).nonzero()[0]
-        res.osd_host_order = int(redo.size)
-        if redo.size:
-            k2 = int(redo.size)
-            host = _pinned(("post", slot), (k2, post_b.shape[1]), torch.float64)
-            # fetch these posteriors with copies that wait only for this
-            # decode's OSD (its event), on a side stream, so the launch stream's
-            # next batch (decode, device OSD) runs during the host's NumPy order
-            side = _side_stream(dev)
-            side.wait_event(ev)
-            if spill is not None and k2 <= spill[3] and int(spill[2][0]) == k2:
-                # the kernels spilled exactly these rows: one contiguous DMA
-                # copy (no gather kernel waiting for free CUs behind other work)
-                sp_post, sp_idx, _, _ = spill
-                idx_h = _pinned(("spill_idx", slot), (k2,), torch.int32)
-                with torch.cuda.stream(side):
-                    host.copy_(sp_post[:k2], non_blocking=True)
-                    idx_h.copy_(sp_idx[:k2], non_blocking=True)
-                side.synchronize()
-                redo = idx_h.numpy().astype(np.int64)
-            else:
-                with torch.cuda.stream(side):
-                    idx_s = torch.as_tensor(redo, device=dev)
-                    host.copy_(post_b.index_select(0, idx_s), non_blocking=True)
-                side.synchronize()
-            idx = torch.as_tensor(redo, device=dev)
-            perm_h = _pinned(("perm", slot), (k2, post_b.shape[1]), torch.int32)
-            perm_h.numpy()[...] = osd_perms(host.numpy())
-            perms = perm_h.to(dev, non_blocking=True)
-            syn_r = syn_b.index_select(0, idx)
-            e_r = e_b.index_select(0, idx)
-            st2 = torch.empty(k2, dtype=torch.int32, device=dev)
-            st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
-            _lib.check(_lib.lib.qldpc_osd_device(code.handle, k2, syn_r.data_ptr(), perms.data_ptr(), int(order),
-                                                 e_r.data_ptr(), st2.data_ptr(), st))
-            e_b.index_copy_(0, idx, e_r)
-            status.index_copy_(0, idx, st2)
-        res.ehat.index_copy_(0, bad, e_b)
-        res.osd_status = status      # checked by the caller (raises IndexError like the reference)
+    with _on_stream(stream):
+        for (H, syn, res), sg in zip(items, staged):
+            if sg is not None:
+                _osd_finish_one(H, syn, res, sg, order)
     return staged
+
+
+def _osd_finish_one(H, syn, res, sg, order):
+    import torch
+    bad, post_b, syn_b, e_b, status, status_h, ev, slot, _, spill = sg
+    dev = res.ehat.device
+    code = _lib.code_for(H, dev.index)
+    ev.synchronize()
+    redo = (status_h.numpy() == 2).nonzero()[0]
+    res.osd_host_order = int(redo.size)
+    if redo.size:
+        k2 = int(redo.size)
+        host = _pinned(("post", slot), (k2, post_b.shape[1]), torch.float64)
+        # fetch these posteriors with copies that wait only for this
+        # decode's OSD (its event), on a side stream, so the launch stream's
+        # next batch (decode, device OSD) runs during the host's NumPy order
+        side = _side_stream(dev)
+        side.wait_event(ev)
+        if spill is not None and k2 <= spill[3] and int(spill[2][0]) == k2:
+            # the kernels spilled exactly these rows: one contiguous DMA
+            # copy (no gather kernel waiting for free CUs behind other work)
+            sp_post, sp_idx, _, _ = spill
+            idx_h = _pinned(("spill_idx", slot), (k2,), torch.int32)
+            with torch.cuda.stream(side):
+                host.copy_(sp_post[:k2], non_blocking=True)
+                idx_h.copy_(sp_idx[:k2], non_blocking=True)
+            side.synchronize()
+            redo = idx_h.numpy().astype(np.int64)
+        else:
+            with torch.cuda.stream(side):
+                idx_s = torch.as_tensor(redo, device=dev)
+                host.copy_(post_b.index_select(0, idx_s), non_blocking=True)
+            side.synchronize()
+        idx = torch.as_tensor(redo, device=dev)
+        perm_h = _pinned(("perm", slot), (k2, post_b.shape[1]), torch.int32)
+        perm_h.numpy()[...] = osd_perms(host.numpy())
+        perms = perm_h.to(dev, non_blocking=True)
+        syn_r = syn_b.index_select(0, idx)
+        e_r = e_b.index_select(0, idx)
+        st2 = torch.empty(k2, dtype=torch.int32, device=dev)
+        st = torch.cuda.current_stream(dev).cuda_stream
+        _lib.check(_lib.lib.qldpc_osd_device(code.handle, k2, syn_r.data_ptr(), perms.data_ptr(), int(order),
+                                             e_r.data_ptr(), st2.data_ptr(), st))
+        e_b.index_copy_(0, idx, e_r)
+        status.index_copy_(0, idx, st2)
+    res.ehat.index_copy_(0, bad, e_b)
+    res.osd_status = status      # checked by the caller (raises IndexError like the reference)
 
 
 def osd_status_check(items, defer=None):

@@ -197,12 +197,6 @@ def _device_ok():
         return False
 
 
-def _grouped_off():
-    """ms_layered_grp_kernel (opt-in, QLDPC_MS_GROUPS > 1) writes byte estimates only."""
-    import os
-    return os.environ.get("QLDPC_MS_GROUPS", "1") in ("", "1")
-
-
 def _channel_ok(Hx, Hz):
     """The device sampler / counters handle n <= 4096 qubits (64 error words
     per shot, qldpc_channel_sample); larger codes use the host sampler."""
@@ -293,7 +287,7 @@ def simulate_p(Hx: np.ndarray, Hz: np.ndarray, p: float, shots: int = 1000, decT
                 B = min(batch_size, my_shots - done)
                 # bit-packed syndromes and estimates (one bit per check / qubit
                 # in HBM) unless OSD needs byte rows of the failing shots
-                packed = osd < 0 and _grouped_off()
+                packed = osd < 0
                 sy_z, sy_x, errX, errZ = ch.sample(p, B, bits=packed)
                 want_post = osd >= 0
                 rX = decoders.decode_batch(Hz, sy_z, p / 3, decIterations, algo=decType, want_post=want_post,
@@ -459,7 +453,15 @@ def _init_dist_from_env():
         return False
     backend = os.environ.get("QLDPC_SIM_BACKEND", "nccl" if torch.cuda.is_available() else "gloo")
     if torch.cuda.is_available():
-        local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        ndev = torch.cuda.device_count()
+        if local >= ndev:
+            if backend == "nccl":
+                # one process per GPU: under RCCL a second rank on a device is
+                # a launch error, not something to fold silently (bench.py too)
+                raise RuntimeError(f"LOCAL_RANK {local} but only {ndev} HIP device(s) visible: launch at "
+                                   "most one rank per GPU (QLDPC_SIM_BACKEND=gloo rehearses more ranks)")
+            local %= max(1, ndev)              # gloo rehearsal: ranks may share a device
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))

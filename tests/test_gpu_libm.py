@@ -1,5 +1,7 @@
 """include/qldpc_libm.h evaluates bit-identically on gfx950 and on the host
-(the property that makes BP GPU-vs-oracle parity exact)."""
+(the property that makes BP GPU == oracle == reference exact): NumPy's tanh
+and SVML's atanh with their tables read from device memory, and the device
+division."""
 import ctypes
 import os
 import subprocess
@@ -14,9 +16,14 @@ pytestmark = pytest.mark.gpu
 HIP_SRC = r'''
 #include <hip/hip_runtime.h>
 #include "qldpc_libm.h"
+__constant__ qldpc_libm_tab tab = QLDPC_LIBM_TAB_INIT;
 __global__ void k(const double* x, double* t, double* a, double* l, long n) {
   long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  if (i < n) { t[i] = qldpc_tanh(x[i]); a[i] = qldpc_atanh(x[i]); l[i] = qldpc_log1p(x[i]); }
+  if (i < n) {
+    t[i] = qldpc_tanh_t(x[i], tab.tanh_c);
+    a[i] = qldpc_atanh_t(x[i], tab.atanh_hl, tab.atanh_rcp);
+    l[i] = qldpc_tanh_t(2.0 * x[i], tab.tanh_c);
+  }
 }
 __global__ void kd(const double* x, const double* y, double* q, long n) {
   long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
@@ -47,7 +54,7 @@ extern "C" int run(const double* hx, double* ht, double* ha, double* hl, long n)
 C_SRC = r'''
 #include "qldpc_libm.h"
 int run(const double* x, double* t, double* a, double* l, long n) {
-  for (long i = 0; i < n; ++i) { t[i] = qldpc_tanh(x[i]); a[i] = qldpc_atanh(x[i]); l[i] = qldpc_log1p(x[i]); }
+  for (long i = 0; i < n; ++i) { t[i] = qldpc_tanh(x[i]); a[i] = qldpc_atanh(x[i]); l[i] = qldpc_tanh(2.0 * x[i]); }
   return 0;
 }
 '''
@@ -74,7 +81,7 @@ def test_libm_bit_identical_gpu_vs_host(tmp_path):
         rc = L.run(P(x), P(t), P(a), P(l), ctypes.c_long(len(x)))
         assert not rc
         outs[name] = (t, a, l)
-    for fn, g, c in zip(("tanh", "atanh", "log1p"), outs["g"], outs["c"]):
+    for fn, g, c in zip(("tanh", "atanh", "tanh(2x)"), outs["g"], outs["c"]):
         bad = np.flatnonzero(g.view(np.uint64) != c.view(np.uint64))
         assert bad.size == 0, f"{fn}: {bad.size} differ, e.g. x={x[bad[:5]]} gpu={g[bad[:5]]} host={c[bad[:5]]}"
 
@@ -82,9 +89,10 @@ def test_libm_bit_identical_gpu_vs_host(tmp_path):
 def test_device_division_is_ieee_in_range(tmp_path):
     """QLDPC_DIV on the device (the compiler's division sequence without the
     v_div_scale / v_div_fixup range steps) equals IEEE a / b bit for bit over
-    the range its callers guarantee: 2^-500 < |a|, |b| < 2^500 or a = 0,
-    including quotients next to 1 (P / t_k), mantissas at the edges of
-    [1, 2) and random exponent pairs."""
+    the range its callers guarantee: 2^-500 < |a|, |b| < 2^500 (a != 0: a
+    -0 numerator would lose its sign without v_div_fixup, so the BP kernels
+    send zero products to the general division), including quotients next to
+    1 (P / t_k), mantissas at the edges of [1, 2) and random exponent pairs."""
     import qldpcsim_amd._lib  # noqa: F401
     inc = os.path.join(ROOT, "include")
     (tmp_path / "g.hip").write_text(HIP_SRC)
@@ -96,11 +104,11 @@ def test_device_division_is_ieee_in_range(tmp_path):
     a = np.concatenate([sgn(N) * rng.uniform(1, 2, N) * 2.0 ** rng.integers(-499, 499, N),
                         sgn(N) * rng.uniform(0, 1, N),
                         np.nextafter(1.0, 0) ** rng.integers(0, 64, N),
-                        np.zeros(1000), 1 + np.arange(1000) * 2.0 ** -52])
+                        1 + np.arange(1000) * 2.0 ** -52])
     b = np.concatenate([sgn(N) * rng.uniform(1, 2, N) * 2.0 ** rng.integers(-499, 499, N),
                         sgn(N) * (1 - rng.uniform(0, 1, N) * 0.999),
                         np.nextafter(1.0, 2) ** rng.integers(0, 64, N),
-                        rng.uniform(0.5, 3, 1000), 2 - np.arange(1000) * 2.0 ** -52])
+                        2 - np.arange(1000) * 2.0 ** -52])
     q = np.empty_like(a)
     L = ctypes.CDLL(str(tmp_path / "g.so"))
     P = lambda v: v.ctypes.data_as(ctypes.c_void_p)

@@ -296,3 +296,31 @@ def test_ordered_osd_spill_matches_status():
     idx = sp_idx[:c].cpu().numpy()
     assert sorted(idx.tolist()) == two.tolist()
     np.testing.assert_array_equal(sp_post[:c].cpu().numpy(), q[idx])
+
+
+def test_apply_osd_device_on_explicit_stream_and_rejects_packed_formats(monkeypatch):
+    """apply_osd_device(..., stream=s) queues every kernel, copy and event on
+    `s` (same result as torch's current stream), and refuses bit-packed
+    decodes (int64 word syndromes / ehat_bits) instead of letting the byte-
+    wide OSD kernels read and write past them."""
+    import torch
+    from qldpcsim_amd import decoders
+    monkeypatch.setenv("QLDPC_OSD_DEVICE_MIN", "1")
+    H, syn, e, post = _decoded_posteriors("LP118_2", 0.1, 600, 30, 13)
+    k = len(syn)
+    d = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a, dt), device="cuda")  # noqa: E731
+    want, _ = _gpu_osd(H, syn, e, post, 0)
+    s = torch.cuda.Stream()
+    res = decoders.DecodeResult(d(e, np.uint8), torch.zeros(k, dtype=torch.int32, device="cuda"),
+                                d(post, np.float64), torch.zeros(k, dtype=torch.int32, device="cuda"))
+    torch.cuda.synchronize()
+    decoders.apply_osd_device(H, d(syn, np.uint8), res, 0, stream=s.cuda_stream)
+    s.synchronize()
+    np.testing.assert_array_equal(res.ehat.cpu().numpy(), want)
+    # bit-packed syndromes / estimates are refused
+    s_bits = decoders.pack_bits(d(syn, np.uint8))
+    with pytest.raises(ValueError):
+        decoders.apply_osd_device(H, s_bits, res, 0)
+    res_b = decoders.DecodeResult(decoders.pack_bits(d(e, np.uint8)), res.iters, res.post, res.flags)
+    with pytest.raises(ValueError):
+        decoders.apply_osd_device(H, d(syn, np.uint8), res_b, 0)

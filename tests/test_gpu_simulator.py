@@ -296,3 +296,18 @@ def test_device_pipeline_counters_exact_on_configs_workload(decType, osd, p, max
     assert got == want
     if decType == "MS":
         assert capped > 50                  # OSD ran on many shots of every batch
+
+
+def test_simulator_refuses_more_ranks_than_gpus_over_rccl(monkeypatch):
+    """Under RCCL one rank per GPU: a LOCAL_RANK past the visible devices is a
+    launch error (raised before the process group forms), as bench.py's; the
+    gloo rehearsal switch still lets ranks share a device."""
+    import torch
+    from qldpcsim_amd import simulator
+    n = torch.cuda.device_count()
+    monkeypatch.setenv("WORLD_SIZE", str(n + 1))
+    monkeypatch.setenv("RANK", str(n))
+    monkeypatch.setenv("LOCAL_RANK", str(n))
+    monkeypatch.delenv("QLDPC_SIM_BACKEND", raising=False)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        simulator._init_dist_from_env()
