@@ -253,7 +253,8 @@ def apply_osd_device_many(items, order, stream=None):
     of a batch): every device order and elimination is queued first."""
     staged = osd_device_stage(items, stream, order=order)
     osd_device_finish(items, staged, order, stream)
-    osd_status_check(items)
+    with _on_stream(stream):                      # the status check reads on the same stream
+        osd_status_check(items)
     return [r.ehat for _, _, r in items]
 
 

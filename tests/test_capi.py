@@ -66,7 +66,8 @@ def test_cpython_set_difference_order_emulation():
         assert _lib.lib.qldpc_cpython_setdiff_first(n, _lib.ptr(J), k) == want
 
 
-OSD = golden_cases("_osd")
+OSD = [(c, a) for c, a in golden_cases("_osd") if c["osd"] >= 0]
+OSD50 = golden_cases("_osd50")
 
 
 @pytest.mark.parametrize("ca", OSD, ids=[f"{c['algo']}-{c['code']}-osd{c['osd']}-{c['id']}" for c, _ in OSD])
@@ -85,6 +86,24 @@ def test_osd_matches_reference_golden(ca):
         if not conv:
             ek = decoders.OSDdec(H, ek, a["syn"][k].astype(int), post[k], c["osd"])
         np.testing.assert_array_equal(ek.astype(np.uint8), a["ehat"][k])
+
+
+@pytest.mark.parametrize("order", [0, 1])
+def test_osd_matches_reference_golden_at_configs3_setting(order):
+    """configs[3]'s setting (LP118_2, MS layered, 50 iterations, p = 0.1):
+    for every non-converged golden shot, the host OSD on the reference's own
+    final posteriors gives the reference's post-OSD estimate (OSD-0 and
+    OSD-1, decoders.py:179-180 -> :299-370). These posteriors carry the exact
+    min-sum ties that drive the GPU order's certification."""
+    from qldpcsim_amd import decoders
+    n_osd = 0
+    for c, a in OSD50:
+        H = half_matrix(c)
+        for k in np.flatnonzero(a["conv"] == 0):
+            ek = decoders.OSDdec(H, a["ehat"][k].astype(np.int8), a["syn"][k].astype(int), a["post"][k], order)
+            np.testing.assert_array_equal(ek.astype(np.uint8), a[f"ehat_osd{order}"][k])
+            n_osd += 1
+    assert n_osd >= 64, n_osd
 
 
 def test_osd_random_matches_oracle_restatement():

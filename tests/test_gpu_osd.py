@@ -324,3 +324,38 @@ def test_apply_osd_device_on_explicit_stream_and_rejects_packed_formats(monkeypa
     res_b = decoders.DecodeResult(decoders.pack_bits(d(e, np.uint8)), res.iters, res.post, res.flags)
     with pytest.raises(ValueError):
         decoders.apply_osd_device(H, d(syn, np.uint8), res_b, 0)
+
+
+@pytest.mark.parametrize("device_min", ["1", "4096"])    # device reliability order / host order
+@pytest.mark.parametrize("order", [0, 1])
+def test_device_osd_pipeline_matches_reference_at_configs3(order, device_min, monkeypatch):
+    """configs[3]'s setting from the reference itself (tests/golden/
+    ms_LP118_2_osd50.npz: LP118_2 MS layered, 50 iterations, p = 0.1): the
+    device decode reproduces the reference's iterations and posteriors, then
+    the full device OSD path — device reliability order with its tie
+    certification, the status-2 host fallback (NumPy's order), block
+    elimination — reproduces the reference's OSD-0 / OSD-1 estimates on every
+    non-converged shot (decoders.py:179-180, :299-370)."""
+    import torch
+    from conftest import golden_cases, half_matrix
+    from qldpcsim_amd import decoders
+    monkeypatch.setenv("QLDPC_OSD_DEVICE_MIN", device_min)
+    n_osd = fallback = 0
+    for c, a in golden_cases("_osd50"):
+        H = half_matrix(c)
+        syn = torch.as_tensor(a["syn"], device="cuda")
+        r = decoders.decode_batch(H, syn, c["p_phys"] / 3, c["max_iter"], algo="MS", want_post=True,
+                                  layer_ptr=a["layer_ptr"], layer_rows=a["layer_rows"])
+        decoders.apply_osd_device(H, syn, r, order)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(r.iters.cpu().numpy(), a["iters"])
+        np.testing.assert_array_equal(r.post.cpu().numpy().view(np.uint64), a["post"].view(np.uint64))
+        conv = a["conv"] != 0
+        np.testing.assert_array_equal(((r.flags.cpu().numpy() & 1) != 0), conv)
+        want = np.where(conv[:, None], a["ehat"], a[f"ehat_osd{order}"])
+        np.testing.assert_array_equal(r.ehat.cpu().numpy(), want)
+        n_osd += int((~conv).sum())
+        fallback += getattr(r, "osd_host_order", 0)
+    assert n_osd >= 64, n_osd
+    if device_min == "1":
+        assert 0 < fallback < n_osd, (fallback, n_osd)    # ties sent some shots to NumPy's order

@@ -58,3 +58,19 @@ def test_oracle_bp100_against_reference():
         short += int((a["iters"] <= 30).sum())
         long_ += int((a["iters"] > 30).sum())
     assert short >= 64 and long_ >= 24, (short, long_)
+
+
+def test_oracle_osd_at_configs3_setting():
+    """The oracle's OSD restatement (oracle.osd_dec) on the reference's final
+    posteriors of configs[3]'s decodes (LP118_2 MS-L 50 it p = 0.1)
+    reproduces the reference's OSD-0 and OSD-1 estimates."""
+    n = 0
+    for c, a in golden_cases("_osd50"):
+        H = half_matrix(c)
+        for k in np.flatnonzero(a["conv"] == 0):
+            for order in (0, 1):
+                got = oracle.osd_dec(H, a["ehat"][k].astype(np.int64), a["syn"][k].astype(np.int64),
+                                     a["post"][k], order)
+                np.testing.assert_array_equal(got.astype(np.uint8), a[f"ehat_osd{order}"][k])
+            n += 1
+    assert n >= 64, n
