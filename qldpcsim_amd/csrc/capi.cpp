@@ -27,6 +27,7 @@
 #include "decoder_kernels.h"
 #include "osd_kernels.h"
 #include "channel_kernels.h"
+#include "hbm_kernels.h"
 
 using qldpc::DecodeArgs;
 
@@ -69,15 +70,23 @@ struct qldpc_code {
   int m = 0, n = 0, E = 0, device = 0;
   int uniform_deg = 0;  // row degree if every row has it, else 0
   int max_row_deg = 0, max_col_deg = 0;
-  int rank = 0;         // GF(2) rank of H (gf2math.rank), for OSD
+  // GF(2) rank of H (gf2math.rank) and column bit-vectors, for OSD only:
+  // built on first use (code_osd_prep), a large code may never need them
+  mutable std::once_flag osd_once;
+  mutable int rank = -1;
   bool zero_col = false;  // H has an all-zero column (GPU OSD: exact REF kernel only)
+  // the LDS-resident kernels' 16-bit tables hold this code (m, n, E <= 65535);
+  // otherwise every decode takes the HBM-resident kernel
+  bool lds_ok = true;
   std::vector<int32_t> row_ptr, col_idx;     // CSR, np.where(H) order
   std::vector<int32_t> vperm, vinv;          // relabeled -> original, original -> relabeled
   std::vector<int32_t> csc_ptr, csc_edge;    // relabeled-variable CSC: CSR edge ids, ascending check
   std::vector<int32_t> edge_pos;             // CSR edge -> CSC position
   int mw = 0;                                // 64-bit words per column bit-vector
-  std::vector<uint64_t> col_bits;            // [n][mw] column j of H (OSD)
+  mutable std::vector<uint64_t> col_bits;    // [n][mw] column j of H (OSD)
   uint16_t* d_vinv = nullptr;
+  // HBM-resident kernel: 32-bit graph tables (relabeled variables)
+  int32_t *d_row_var = nullptr, *d_row_pos = nullptr, *d_col_ptr = nullptr, *d_vinv32 = nullptr;
   int32_t *d_row_ptr = nullptr, *d_col_idx = nullptr;  // CSR for the GPU OSD
   // layered MS stop-test filters (ms_layered_kernel): 32 fixed random parity
   // checks of H's rows; wc[c] bit k = row c in check k, avar[v] bit k = parity
@@ -105,7 +114,6 @@ extern "C" int qldpc_code_create(const uint8_t* h_H, int m, int n, qldpc_code** 
   if (!out) return fail(QLDPC_EINVAL, "out is null");
   *out = nullptr;
   if (m < 0 || n < 0 || (m * (int64_t)n > 0 && !h_H)) return fail(QLDPC_EINVAL, "bad shape %d x %d", m, n);
-  if (m > 65535 || n > 65535) return fail(QLDPC_EUNSUP, "matrix %d x %d exceeds 65535 rows/columns", m, n);
   auto* c = new qldpc_code();
   c->m = m;
   c->n = n;
@@ -121,10 +129,7 @@ extern "C" int qldpc_code_create(const uint8_t* h_H, int m, int n, qldpc_code** 
     c->row_ptr[r + 1] = (int32_t)c->col_idx.size();
   }
   c->E = (int)c->col_idx.size();
-  if (c->E > 65535) {
-    delete c;
-    return fail(QLDPC_EUNSUP, "%d edges exceed the 65535-edge limit of the 16-bit graph tables", (int)c->col_idx.size());
-  }
+  c->lds_ok = m <= 65535 && n <= 65535 && c->E <= 65535;
   std::vector<int> cdeg(n, 0);
   for (int e = 0; e < c->E; ++e) cdeg[c->col_idx[e]]++;
   for (int r = 0; r < m; ++r) c->max_row_deg = std::max(c->max_row_deg, c->row_ptr[r + 1] - c->row_ptr[r]);
@@ -152,13 +157,7 @@ extern "C" int qldpc_code_create(const uint8_t* h_H, int m, int n, qldpc_code** 
       c->csc_edge[pos] = e;
       c->edge_pos[e] = pos;
     }
-  // column bit-vectors for OSD
   c->mw = (m + 63) / 64;
-  c->col_bits.assign((size_t)n * std::max(c->mw, 1), 0);
-  for (int r = 0; r < m; ++r)
-    for (int e = c->row_ptr[r]; e < c->row_ptr[r + 1]; ++e)
-      c->col_bits[(size_t)c->col_idx[e] * c->mw + (r >> 6)] |= 1ull << (r & 63);
-  c->rank = gf2_rank_cols(c->col_bits, n, c->mw);
   for (int j = 0; j < n && !c->zero_col; ++j) c->zero_col = cdeg[j] == 0;
   c->wc.resize(m);
   for (int r = 0; r < m; ++r) {
@@ -172,9 +171,27 @@ extern "C" int qldpc_code_create(const uint8_t* h_H, int m, int n, qldpc_code** 
     for (int e = c->row_ptr[r]; e < c->row_ptr[r + 1]; ++e) c->avar[c->vinv[c->col_idx[e]]] ^= c->wc[r];
   for (int v = 0; v < n; ++v) c->filt_all ^= c->avar[v];
   if (n > 0 && c->device >= 0) {
-    std::vector<uint16_t> v16(c->vinv.begin(), c->vinv.end());
-    hipError_t e1 = hipMalloc(&c->d_vinv, sizeof(uint16_t) * n);
-    if (e1 == hipSuccess) e1 = hipMemcpy(c->d_vinv, v16.data(), sizeof(uint16_t) * n, hipMemcpyHostToDevice);
+    hipError_t e1 = hipSuccess;
+    if (c->lds_ok) {
+      std::vector<uint16_t> v16(c->vinv.begin(), c->vinv.end());
+      e1 = hipMalloc(&c->d_vinv, sizeof(uint16_t) * n);
+      if (e1 == hipSuccess) e1 = hipMemcpy(c->d_vinv, v16.data(), sizeof(uint16_t) * n, hipMemcpyHostToDevice);
+    }
+    {  // HBM-resident kernel tables
+      std::vector<int32_t> rv(std::max(c->E, 1)), rp(std::max(c->E, 1));
+      for (int e = 0; e < c->E; ++e) {
+        rv[e] = c->vinv[c->col_idx[e]];
+        rp[e] = c->edge_pos[e];
+      }
+      auto up = [&](int32_t** d, const int32_t* h, size_t cnt) {
+        if (e1 == hipSuccess) e1 = hipMalloc(d, sizeof(int32_t) * std::max<size_t>(cnt, 1));
+        if (e1 == hipSuccess && cnt) e1 = hipMemcpy(*d, h, sizeof(int32_t) * cnt, hipMemcpyHostToDevice);
+      };
+      up(&c->d_row_var, rv.data(), c->E);
+      up(&c->d_row_pos, rp.data(), c->E);
+      up(&c->d_col_ptr, c->csc_ptr.data(), n + 1);
+      up(&c->d_vinv32, c->vinv.data(), n);
+    }
     if (e1 == hipSuccess) e1 = hipMalloc(&c->d_row_ptr, sizeof(int32_t) * (m + 1));
     if (e1 == hipSuccess) e1 = hipMemcpy(c->d_row_ptr, c->row_ptr.data(), sizeof(int32_t) * (m + 1), hipMemcpyHostToDevice);
     if (e1 == hipSuccess) e1 = hipMalloc(&c->d_col_idx, sizeof(int32_t) * std::max(1, c->E));
@@ -225,6 +242,10 @@ extern "C" int qldpc_code_destroy(qldpc_code* code) {
   (void)hipFree(code->d_wc);
   (void)hipFree(code->d_rtab);
   (void)hipFree(code->d_avar);
+  (void)hipFree(code->d_row_var);
+  (void)hipFree(code->d_row_pos);
+  (void)hipFree(code->d_col_ptr);
+  (void)hipFree(code->d_vinv32);
   ws_free(code);
   if (code->ws_stream) (void)hipStreamDestroy(code->ws_stream);
   delete code;
@@ -279,6 +300,16 @@ struct qldpc_schedule {
   int f_off_tab = 0;
   LaunchCfg cfg[2];           // per algo
   std::mutex mu;
+  // HBM-resident kernel (hbm_kernels.hip): 32-bit layer tables and a grow-only
+  // slot-major workspace; hbm_ev orders launches that share the workspace
+  bool lds_ok = true;         // the LDS kernels' 16-bit layer tables hold this schedule
+  bool hbm_lazy = false;      // every row in exactly one layer (no state init pass)
+  std::vector<int32_t> h_lay_ptr, h_lay_rows, h_adj_ptr, h_adj_vars, h_fl_var, h_fl_pos;
+  int32_t *d_h_lay_ptr = nullptr, *d_h_lay_rows = nullptr, *d_h_adj_ptr = nullptr, *d_h_adj_vars = nullptr,
+          *d_h_fl_var = nullptr, *d_h_fl_pos = nullptr;
+  void* hbm_ws = nullptr;
+  size_t hbm_ws_bytes = 0;
+  hipEvent_t hbm_ev = nullptr;
   // half-shot work-queue counters (ring: concurrent launches on different
   // streams take different slots; each is zeroed on the launch stream)
   static constexpr int kQueueSlots = 64;
@@ -310,16 +341,16 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
   if (n_layers < 0 || (n_layers > 0 && !h_layer_ptr)) return fail(QLDPC_EINVAL, "bad layer list");
   const int m = code->m, n = code->n;
   std::vector<std::vector<int>> layers(n_layers);
+  std::vector<int> seen(m, -1);
   for (int l = 0; l < n_layers; ++l) {
     const int a = h_layer_ptr[l], b = h_layer_ptr[l + 1];
     if (a < 0 || b < a) return fail(QLDPC_EINVAL, "layer_ptr is not non-decreasing at layer %d", l);
-    std::vector<char> seen(m, 0);
     for (int q = a; q < b; ++q) {
       const int r = h_layer_rows[q];
       if (r < 0 || r >= m)
         return fail(QLDPC_ERANGE, "index %d is out of bounds for axis 0 with size %d", r, m);
-      if (!seen[r]) {  // duplicates inside a layer: same Jacobi inputs, same outputs
-        seen[r] = 1;
+      if (seen[r] != l) {  // duplicates inside a layer: same Jacobi inputs, same outputs
+        seen[r] = l;
         layers[l].push_back(r);
       }
     }
@@ -330,6 +361,47 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
   // One layer holding every row exactly once == flooding (decoders.py:122).
   s->layered = !(n_layers == 1 && (int)layers[0].size() == m);
 
+  // HBM-resident kernel tables (32-bit, every schedule): layer rows, each
+  // layer's adjacent variables (ascending), and for the no-init first
+  // iteration the first layer that reaches each variable / CSC position
+  {
+    s->h_lay_ptr.assign(n_layers + 1, 0);
+    s->h_adj_ptr.assign(n_layers + 1, 0);
+    s->h_fl_var.assign(std::max(n, 1), n_layers);
+    s->h_fl_pos.assign(std::max(code->E, 1), n_layers);
+    std::vector<int> row_layer(m, -1), mark(n, -1);
+    bool part = true;
+    for (int l = 0; l < n_layers; ++l) {
+      std::vector<int> adj;
+      for (int r : layers[l]) {
+        s->h_lay_rows.push_back(r);
+        if (row_layer[r] >= 0) part = false;          // a row in two layers
+        row_layer[r] = l;
+        for (int e = code->row_ptr[r]; e < code->row_ptr[r + 1]; ++e) {
+          const int v = code->vinv[code->col_idx[e]];
+          if (mark[v] != l) {
+            mark[v] = l;
+            adj.push_back(v);
+          }
+        }
+      }
+      std::sort(adj.begin(), adj.end());
+      for (int v : adj) {
+        s->h_adj_vars.push_back(v);
+        s->h_fl_var[v] = std::min(s->h_fl_var[v], l);
+      }
+      s->h_lay_ptr[l + 1] = (int32_t)s->h_lay_rows.size();
+      s->h_adj_ptr[l + 1] = (int32_t)s->h_adj_vars.size();
+    }
+    for (int r = 0; r < m; ++r) {
+      if (row_layer[r] < 0) part = false;             // a row no layer updates
+      for (int e = code->row_ptr[r]; e < code->row_ptr[r + 1]; ++e) s->h_fl_pos[code->edge_pos[e]] = row_layer[r];
+    }
+    s->hbm_lazy = part;
+  }
+  s->lds_ok = code->lds_ok && s->h_lay_rows.size() <= 65535 && s->h_adj_vars.size() <= 65535;
+
+  if (s->lds_ok) {
   std::vector<uint32_t> cn_tab;
   if (fast_table_ok(code)) {
     // uniform row degree: rows padded to 8 entries, pre-scaled LDS byte offsets
@@ -481,6 +553,7 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
       s->fblob.resize(align16((int)s->fblob.size() + 1));
     }
   }
+  }  // s->lds_ok
   s->blob.resize(align16((int)s->blob.size() + 1));
   if (code->device < 0) {  // no device: keep the host image only
     *out = s;
@@ -501,6 +574,16 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
     e1 = hipMalloc(&s->d_lblob, s->lblob.size());
     if (e1 == hipSuccess) e1 = hipMemcpy(s->d_lblob, s->lblob.data(), s->lblob.size(), hipMemcpyHostToDevice);
   }
+  auto up32 = [&](int32_t** d, const std::vector<int32_t>& h) {
+    if (e1 == hipSuccess) e1 = hipMalloc(d, sizeof(int32_t) * std::max<size_t>(h.size(), 1));
+    if (e1 == hipSuccess && !h.empty()) e1 = hipMemcpy(*d, h.data(), sizeof(int32_t) * h.size(), hipMemcpyHostToDevice);
+  };
+  up32(&s->d_h_lay_ptr, s->h_lay_ptr);
+  up32(&s->d_h_lay_rows, s->h_lay_rows);
+  up32(&s->d_h_adj_ptr, s->h_adj_ptr);
+  up32(&s->d_h_adj_vars, s->h_adj_vars);
+  up32(&s->d_h_fl_var, s->h_fl_var);
+  up32(&s->d_h_fl_pos, s->h_fl_pos);
   if (e1 != hipSuccess) {
     delete s;
     return fail(QLDPC_EHIP, "uploading the schedule failed: %s", hipGetErrorString(e1));
@@ -516,6 +599,10 @@ extern "C" int qldpc_schedule_destroy(qldpc_schedule* s) {
   (void)hipFree(s->d_lgblob);
   (void)hipFree(s->d_fblob);
   (void)hipFree(s->d_queue);
+  for (int32_t* d : {s->d_h_lay_ptr, s->d_h_lay_rows, s->d_h_adj_ptr, s->d_h_adj_vars, s->d_h_fl_var, s->d_h_fl_pos})
+    (void)hipFree(d);
+  (void)hipFree(s->hbm_ws);
+  if (s->hbm_ev) (void)hipEventDestroy(s->hbm_ev);
   delete s;
   return QLDPC_OK;
 }
@@ -720,6 +807,125 @@ extern "C" int qldpc_timing_read(double* total_ms, int64_t* launches) {
 // ---------------------------------------------------------------------------
 // decode
 // ---------------------------------------------------------------------------
+// Which kernel family decodes (schedule, algo): the LDS-resident kernels when
+// their tables and per-half-shot state fit, else the HBM-resident kernel
+// (hbm_kernels.hip). QLDPC_FORCE_HBM=1 takes the HBM kernel for any code
+// (tests: the two families agree bit for bit).
+static int choose_path(qldpc_schedule* s, int algo, LaunchCfg** cfg, bool* hbm) {
+  const qldpc_code* c = s->code;
+  const char* ev = getenv("QLDPC_FORCE_HBM");
+  *hbm = !s->lds_ok || (ev && atoi(ev) != 0) || (algo == QLDPC_ALGO_MS && c->max_row_deg > 32) ||
+         (algo == QLDPC_ALGO_BP && c->max_col_deg > 128);
+  if (*hbm) return QLDPC_OK;
+  const int rc = launch_config(s, algo, cfg);
+  if (rc == QLDPC_EUNSUP) {                      // LDS image / state does not fit a CU
+    *hbm = true;
+    return QLDPC_OK;
+  }
+  return rc;
+}
+
+static void record_timing(hipEvent_t e0, hipEvent_t e1);
+
+// The HBM-resident decode: slots = min(batch, 8 waves per CU, what a 16 GiB
+// (or half the free memory) workspace holds); the workspace belongs to the
+// schedule and an event orders launches that share it.
+static int decode_hbm(const qldpc_code* code, qldpc_schedule* s, int algo, const void* d_syn, int syn_format,
+                      int64_t batch, double p, int max_iter, double beta, double eps, void* d_ehat,
+                      int ehat_format, int32_t* d_iters, double* d_post, int32_t* d_flags, hipStream_t st) {
+  const char* name = nullptr;
+  const void* kern = qldpc::select_hbm_kernel(algo, code->max_row_deg, &name);
+  if (!kern) return fail(QLDPC_EUNSUP, "row degree %d exceeds the HBM kernel's 64", code->max_row_deg);
+  int dev = 0, cus = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const size_t w = algo == QLDPC_ALGO_MS ? 4 : 8;
+  const size_t per_slot = (size_t)code->E * w + (size_t)code->n * 8 + (size_t)code->m + 64;
+  std::lock_guard<std::mutex> lk(s->mu);
+  size_t free_b = 0, total_b = 0;
+  HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+  const size_t budget = std::min<size_t>(free_b / 2 + s->hbm_ws_bytes, (size_t)16 << 30);
+  int64_t T = std::min<int64_t>((batch + 255) / 256 * 256, (int64_t)cus * 8 * 64);
+  T = std::min<int64_t>(T, (int64_t)(budget / per_slot) / 256 * 256);
+  if (T < 256) return fail(QLDPC_EUNSUP, "HBM decode needs %zu B per half-shot slot: device memory too small", per_slot);
+  const size_t off_post = (size_t)T * code->E * w;
+  const size_t off_syn = off_post + (size_t)T * code->n * 8;
+  const size_t need = off_syn + (size_t)T * code->m + 256;
+  if (!s->hbm_ev) HIP_TRY(hipEventCreateWithFlags(&s->hbm_ev, hipEventDisableTiming));
+  if (need > s->hbm_ws_bytes) {
+    if (s->hbm_ws) {
+      HIP_TRY(hipEventSynchronize(s->hbm_ev));      // last launch done with the old workspace
+      HIP_TRY(hipFree(s->hbm_ws));
+      s->hbm_ws = nullptr;
+      s->hbm_ws_bytes = 0;
+    }
+    HIP_TRY(hipMalloc(&s->hbm_ws, need));
+    s->hbm_ws_bytes = need;
+  }
+  HIP_TRY(hipStreamWaitEvent(st, s->hbm_ev, 0));    // a launch on another stream may still use it
+  qldpc::HbmArgs a{};
+  a.row_ptr = code->d_row_ptr;
+  a.row_var = code->d_row_var;
+  a.row_pos = code->d_row_pos;
+  a.col_ptr = code->d_col_ptr;
+  a.vinv = code->d_vinv32;
+  a.wc = code->d_wc;
+  a.avar = code->d_avar;
+  a.filt_all = code->filt_all;
+  a.lay_ptr = s->d_h_lay_ptr;
+  a.lay_rows = s->d_h_lay_rows;
+  a.adj_ptr = s->d_h_adj_ptr;
+  a.adj_vars = s->d_h_adj_vars;
+  a.n_layers = s->n_layers;
+  a.m = code->m;
+  a.n = code->n;
+  a.E = code->E;
+  a.c2v = s->hbm_ws;
+  a.post = (double*)((char*)s->hbm_ws + off_post);
+  a.synT = (uint8_t*)s->hbm_ws + off_syn;
+  a.T = T;
+  a.syn = (const uint8_t*)d_syn;
+  a.ehat = (uint8_t*)d_ehat;
+  a.iters = d_iters;
+  a.out_post = d_post;
+  a.flags = d_flags;
+  a.syn_bits = syn_format == QLDPC_FMT_BITS;
+  a.eh_bits = ehat_format == QLDPC_FMT_BITS;
+  a.wm = (code->m + 63) / 64;
+  a.wn = (code->n + 63) / 64;
+  a.batch = batch;
+  a.queue = s->d_queue + (s->qnext.fetch_add(1) % qldpc_schedule::kQueueSlots);
+  a.L = qldpc_prior_llr(p, eps);                    // np.log prior (decoders.py:147, :232)
+  a.L32 = (float)a.L;
+  a.beta = beta;
+  a.eps = eps;
+  a.max_iter = max_iter;
+  HIP_TRY(hipMemsetAsync(a.queue, 0, sizeof(uint32_t), st));
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  bool timed;
+  {
+    std::lock_guard<std::mutex> tk(g_tmu);
+    timed = g_timing;
+  }
+  if (timed) {
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipEventRecord(e0, st));
+  }
+  HIP_TRY(qldpc::launch_hbm(kern, a, (int)(T / 256), 256, s->d_h_fl_var, s->d_h_fl_pos, s->hbm_lazy ? 1 : 0, st));
+  if (timed) {
+    HIP_TRY(hipEventRecord(e1, st));
+    record_timing(e0, e1);
+  }
+  HIP_TRY(hipEventRecord(s->hbm_ev, st));
+  return QLDPC_OK;
+}
+
+static void record_timing(hipEvent_t e0, hipEvent_t e1) {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  g_events.emplace_back(e0, e1);
+}
+
 extern "C" int qldpc_decode_device(const qldpc_code* code, const qldpc_schedule* sched_c, int algo,
                                    const uint8_t* d_syn, int64_t batch, double p, int max_iter,
                                    double beta, double eps, uint8_t* d_ehat, int32_t* d_iters,
@@ -743,17 +949,17 @@ extern "C" int qldpc_decode_device_ex(const qldpc_code* code, const qldpc_schedu
   if (max_iter < 1) return fail(QLDPC_EINVAL, "max_iter must be >= 1 (the reference leaves e_hat unbound)");
   if (batch == 0) return QLDPC_OK;
   if (!d_syn || !d_ehat || !d_iters) return fail(QLDPC_EINVAL, "null device buffer");
-  if (algo == QLDPC_ALGO_MS && code->max_row_deg > 32)
-    return fail(QLDPC_EUNSUP, "min-sum kernel supports row degree <= 32 (got %d)", code->max_row_deg);
-  if (algo == QLDPC_ALGO_BP && code->max_col_deg > 128)
-    return fail(QLDPC_EUNSUP, "BP kernel supports column degree <= 128 (got %d)", code->max_col_deg);
   if (code->device < 0 || !sched->d_blob) return fail(QLDPC_EHIP, "no HIP device was visible when the code/schedule was created");
   int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
   if (dev != code->device) return fail(QLDPC_EINVAL, "code lives on device %d, current device is %d", code->device, dev);
   LaunchCfg* cfg = nullptr;
-  int rc = launch_config(sched, algo, &cfg);
+  bool hbm = false;
+  int rc = choose_path(sched, algo, &cfg, &hbm);
   if (rc) return rc;
+  if (hbm)
+    return decode_hbm(code, sched, algo, d_syn, syn_format, batch, p, max_iter, beta, eps, d_ehat, ehat_format,
+                      d_iters, d_post, d_flags, (hipStream_t)stream);
 
   DecodeArgs a{};
   a.blob = sched->d_blob;
@@ -872,9 +1078,13 @@ extern "C" int qldpc_decode_kernel_name(const qldpc_code* code, const qldpc_sche
   if (algo != QLDPC_ALGO_MS && algo != QLDPC_ALGO_BP) return fail(QLDPC_EINVAL, "Unrecognized decoder type.");
   if (code->device < 0 || !sched->d_blob) return fail(QLDPC_EHIP, "no HIP device was visible when the code/schedule was created");
   LaunchCfg* cfg = nullptr;
-  int rc = launch_config(sched, algo, &cfg);
+  bool hbm = false;
+  int rc = choose_path(sched, algo, &cfg, &hbm);
   if (rc) return rc;
-  snprintf(buf, (size_t)len, "%s", cfg->name);
+  const char* hname = nullptr;
+  if (hbm && !qldpc::select_hbm_kernel(algo, code->max_row_deg, &hname))
+    return fail(QLDPC_EUNSUP, "row degree %d exceeds the HBM kernel's 64", code->max_row_deg);
+  snprintf(buf, (size_t)len, "%s", hbm ? hname : cfg->name);
   return QLDPC_OK;
 }
 
@@ -967,6 +1177,17 @@ static int gf2_rank_cols(const std::vector<uint64_t>& cols, int n, int mw) {
   return r;
 }
 
+// OSD's column bit-vectors and rank(H), built once on first OSD use
+static void code_osd_prep(const qldpc_code* c) {
+  std::call_once(c->osd_once, [c] {
+    c->col_bits.assign((size_t)c->n * std::max(c->mw, 1), 0);
+    for (int r = 0; r < c->m; ++r)
+      for (int e = c->row_ptr[r]; e < c->row_ptr[r + 1]; ++e)
+        c->col_bits[(size_t)c->col_idx[e] * c->mw + (r >> 6)] |= 1ull << (r & 63);
+    c->rank = gf2_rank_cols(c->col_bits, c->n, c->mw);
+  });
+}
+
 // Order of iteration of CPython's `set(range(n)) - set(J)` (the reference's
 // infoSet, decoders.py:344): returns its first element. Emulates
 // setobject.c (set_difference -> set_add_entry / set_table_resize /
@@ -1052,6 +1273,7 @@ static int osd_one(const qldpc_code* c, const uint8_t* syn, const int32_t* perm,
                    int32_t* J_out, int32_t* J_size, int first_info_index) {
   const int m = c->m, n = c->n, mw = c->mw;
   if (n == 0) return QLDPC_OK;
+  code_osd_prep(c);
   // (1) least reliable basis J (decoders.py:329-342): index 0 unconditionally,
   //     then every column (in perm order) that raises the rank, until rank(H).
   Gf2Basis B(std::max(mw * 64, 1), mw);
@@ -1265,6 +1487,7 @@ extern "C" int qldpc_osd_device_ordered_ex(const qldpc_code* code, int64_t count
 static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t* d_syn, const int32_t* d_perm,
                            const int32_t* d_tiepos, const double* d_post, int order, uint8_t* d_ehat,
                            int32_t* d_status, void* stream) {
+  if (code) code_osd_prep(code);
   if (!code) return fail(QLDPC_EINVAL, "code is null");
   if (count < 0) return fail(QLDPC_EINVAL, "negative count");
   if (count == 0) return QLDPC_OK;

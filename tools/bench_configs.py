@@ -62,6 +62,49 @@ def run(code, algo, sched, p, max_iter, B, reps=2):
             "shots_per_s_wall": reps * B / wall, "avg_iters": its / (2 * reps * B)}
 
 
+def run_hbm(n, dv, dc, algo, p, max_iter, B, force_code=None):
+    """The HBM-resident kernel: a synthetic (dv, dc)-regular code of n
+    variables (or a bundled code with QLDPC_FORCE_HBM), one launch per half;
+    achieved GB/s under SURVEY.md 8(d)'s streaming model, w(3E + 2n) bytes
+    per executed half-shot iteration (w = 4 MS / 8 BP), against 8 TB/s."""
+    if force_code:
+        os.environ["QLDPC_FORCE_HBM"] = "1"
+        Hx, Hz = codes.load_code(force_code)
+        H = Hz
+    else:
+        rng = np.random.default_rng(1)
+        m = n * dv // dc
+        H = np.zeros((m, n), np.uint8)
+        H[rng.permutation(np.repeat(np.arange(m), dc)), np.repeat(np.arange(n), dv)] = 1
+    m, n = H.shape
+    E = int(H.sum())
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    if p is None:
+        s = torch.randint(0, 2, (B, m), dtype=torch.uint8, device="cuda", generator=gen)
+        prior = 0.05 / 3
+    else:
+        e = (torch.rand((B, n), device="cuda", generator=gen) < p).half()
+        s = (e @ torch.as_tensor(H.T, dtype=torch.half, device="cuda")).remainder_(2).to(torch.uint8)
+        prior = p / 3
+    lp, lr = np.array([0, m], np.int32), np.arange(m, dtype=np.int32)
+    name = _lib.kernel_name(H, lp, lr, algo)
+    decoders.decode_batch(H, s[:256], prior, max_iter, algo=algo, layer_ptr=lp, layer_rows=lr)
+    torch.cuda.synchronize()
+    _lib.timing_enable(True)
+    _lib.timing_reset()
+    r = decoders.decode_batch(H, s, prior, max_iter, algo=algo, layer_ptr=lp, layer_rows=lr)
+    its = int(r.iters.sum().item())
+    ms, nl = _lib.timing_read()
+    _lib.timing_enable(False)
+    os.environ.pop("QLDPC_FORCE_HBM", None)
+    w = 4 if algo == "MS" else 8
+    byts = its * (w * (3 * E + 2 * n)) + B * (m + n + 4)
+    return {"hbm_kernel": name, "code": force_code or f"regular({dv},{dc}) n={n}", "m": m, "n": n, "E": E,
+            "algo": algo, "p": p, "max_iter": max_iter, "batch": B, "kernel_ms": ms / nl,
+            "half_shots_per_s": B / (ms / 1e3), "avg_iters": its / B,
+            "algorithmic_gbs": byts / (ms / 1e3) / 1e9, "hbm_frac": byts / (ms / 1e3) / 1e9 / 8000.0}
+
+
 def run_osd(code, count, order=0):
     """GPU OSD throughput on random posteriors / arbitrary syndromes."""
     Hx, Hz = codes.load_code(code)
@@ -102,6 +145,11 @@ def main():
         ("LP118_2", "MS", "F", None, 50, S),
         ("LP118_2", "BP", "L", 0.05, 100, S // 2),           # configs[4] (decoder part)
     ]
+    if "--hbm" in sys.argv:
+        for pt in [(16384, 3, 6, "MS", None, 50, 16384), (16384, 3, 6, "MS", 0.02, 50, 65536),
+                   (16384, 3, 6, "BP", None, 20, 8192), (None, None, None, "MS", None, 50, 65536, "LP118_0")]:
+            print(json.dumps(run_hbm(*pt)), flush=True)
+        return
     if "--osd" in sys.argv:
         for c in ("LP04_0", "LP118_0", "LP118_2"):
             print(json.dumps(run_osd(c, 8192)), flush=True)
