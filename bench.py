@@ -19,9 +19,10 @@ synchronize; elapsed time is the max over ranks; `value` = all ranks' shots /
 that time.
 
 `roofline` prices the decode kernel against the on-chip unit that binds it
-(DESIGN.md §3.3): VALU issue (one wave64 VALU instruction per SIMD per 4
-cycles — the SQ's quad-cycle accounting — 1024 SIMDs at 2.4 GHz) or the LDS
-array (one cycle per CU per LDS array cycle, 256 CUs at 2.4 GHz). Per-unit
+(DESIGN.md §5): VALU issue time by instruction class (a wave64 32-bit VALU op
+occupies a SIMD-32 for 2 cycles, a float64 add / mul / fma 4, transcendentals
+8 / 16; 1024 SIMDs at 2.4 GHz) or the LDS array (one cycle per CU per LDS
+array cycle, 256 CUs at 2.4 GHz). Per-unit
 instruction / LDS-cycle / HBM-byte counts come from a committed rocprofv3
 profile of the same kernel build (profiles/*_roofline.json, matched by kernel
 name and by the hash of the library's device code object), multiplied by this
@@ -435,12 +436,20 @@ def roofline(names, t_launch, hs_launch, it_launch, algo_launch, launches):
                      "(tools/gpu_profile_roofline.sh regenerates it): bound and frac unmeasured")
         return r
     pu = prof["per_half_shot_iteration"]
-    valu = pu["valu_insts"] * it_launch / t_launch / 1e9             # G wave-instructions / s
-    valu_peak = SIMDS * CLOCK_GHZ / VALU_CYCLES
+    if "valu_cycles" in pu:
+        # VALU issue time by instruction class (32-bit ops 2 cycles per wave64
+        # on a SIMD-32, float64 add/mul/fma 4, transcendentals 8/16), per SIMD
+        valu = pu["valu_cycles"] * it_launch / t_launch / 1e9            # G SIMD-cycles / s
+        valu_peak = SIMDS * CLOCK_GHZ
+        valu_unit = "G SIMD VALU-issue cycles/s (class-weighted)"
+    else:
+        valu = pu["valu_insts"] * it_launch / t_launch / 1e9             # G wave-instructions / s
+        valu_peak = SIMDS * CLOCK_GHZ / VALU_CYCLES
+        valu_unit = "G VALU wave-instructions/s (4 cycles each)"
     lds = pu["lds_cycles"] * it_launch / t_launch / 1e9              # G LDS-array cycles / s (chip)
     lds_peak = CUS * CLOCK_GHZ
     traffic = prof["per_half_shot"]["hbm_bytes"] * hs_launch
-    units = {"valu": {"achieved": valu, "peak": valu_peak, "unit": "G VALU wave-instructions/s",
+    units = {"valu": {"achieved": valu, "peak": valu_peak, "unit": valu_unit,
                       "frac": valu / valu_peak},
              "lds": {"achieved": lds, "peak": lds_peak, "unit": "G LDS-array cycles/s (all CUs)",
                      "frac": lds / lds_peak}}
@@ -448,8 +457,9 @@ def roofline(names, t_launch, hs_launch, it_launch, algo_launch, launches):
     r.update(bound=bound, achieved=units[bound]["achieved"], peak=units[bound]["peak"],
              unit=units[bound]["unit"], frac=units[bound]["frac"], traffic=traffic, units=units)
     r["hbm"].update(achieved_gbs=traffic / t_launch / 1e9, frac=traffic / t_launch / 1e9 / HBM_PEAK_GBS)
-    r["formula"] = ("valu frac = valu_insts/half-shot-iter x iterations/launch x 4 cycles / "
-                    "(1024 SIMDs x 2.4 GHz x launch time); lds frac = lds_cycles/half-shot-iter x "
+    r["formula"] = ("valu frac = valu_cycles/half-shot-iter x iterations/launch / (1024 SIMDs x 2.4 GHz x "
+                    "launch time), valu_cycles = 2 x SQ_INSTS_VALU + 2 x (ADD+MUL+FMA_F64) + 14 x TRANS_F64 + "
+                    "6 x TRANS_F32 (per-class SQ_INSTS_VALU_* counters); lds frac = lds_cycles/half-shot-iter x "
                     "iterations/launch / (256 CUs x 2.4 GHz x launch time); per-unit counts from the "
                     "profile (SQ_INSTS_VALU, SQ_LDS_IDX_ACTIVE; traffic = 2 x FETCH_SIZE + WRITE_SIZE), "
                     "launch time and iterations from this run")

@@ -827,7 +827,7 @@ static int choose_path(qldpc_schedule* s, int algo, LaunchCfg** cfg, bool* hbm) 
 
 static void record_timing(hipEvent_t e0, hipEvent_t e1);
 
-// The HBM-resident decode: slots = min(batch, 8 waves per CU, what a 16 GiB
+// The HBM-resident decode: slots = min(batch, 16 waves per CU, what a 64 GiB
 // (or half the free memory) workspace holds); the workspace belongs to the
 // schedule and an event orders launches that share it.
 static int decode_hbm(const qldpc_code* code, qldpc_schedule* s, int algo, const void* d_syn, int syn_format,
@@ -844,8 +844,8 @@ static int decode_hbm(const qldpc_code* code, qldpc_schedule* s, int algo, const
   std::lock_guard<std::mutex> lk(s->mu);
   size_t free_b = 0, total_b = 0;
   HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-  const size_t budget = std::min<size_t>(free_b / 2 + s->hbm_ws_bytes, (size_t)16 << 30);
-  int64_t T = std::min<int64_t>((batch + 255) / 256 * 256, (int64_t)cus * 8 * 64);
+  const size_t budget = std::min<size_t>(free_b / 2 + s->hbm_ws_bytes, (size_t)64 << 30);
+  int64_t T = std::min<int64_t>((batch + 255) / 256 * 256, (int64_t)cus * 16 * 64);
   T = std::min<int64_t>(T, (int64_t)(budget / per_slot) / 256 * 256);
   if (T < 256) return fail(QLDPC_EUNSUP, "HBM decode needs %zu B per half-shot slot: device memory too small", per_slot);
   const size_t off_post = (size_t)T * code->E * w;

@@ -62,6 +62,8 @@ template <int ALGO, int DCMAX>
 __global__ void __launch_bounds__(256) hbm_decode_kernel(HbmArgs a, const int32_t* __restrict__ fl_var,
                                                        const int32_t* __restrict__ fl_pos, int lazy) {
   using Msg = typename std::conditional<ALGO == ALGO_MS, float, double>::type;
+  constexpr int UC = DCMAX <= 8 ? (ALGO == ALGO_MS ? 4 : 2) : (DCMAX <= 16 ? 2 : 1);   // checks per load batch
+  constexpr int UV = 4, KV = 8;                   // variables per load batch, messages loaded up front
   const qldpc_libm_tab* lt = nullptr;
   if constexpr (ALGO == ALGO_BP) {
     __shared__ qldpc_libm_tab lt_s;
@@ -81,7 +83,7 @@ __global__ void __launch_bounds__(256) hbm_decode_kernel(HbmArgs a, const int32_
 
   long long shot = -1;
   bool need = true;          // take a half-shot at the next iteration boundary
-  int it = 0, fl = 0;
+  int it = 0, fl = 0, lstop = 0;
   uint32_t F = 0, B = 0;
 
   for (;;) {
@@ -129,102 +131,146 @@ __global__ void __launch_bounds__(256) hbm_decode_kernel(HbmArgs a, const int32_
     for (int l = 0; l < a.n_layers; ++l) {
       const bool act = shot >= 0 && !stop;
       const bool first = it == 0;
-      // check nodes of the layer (Jacobi: all read the same posteriors)
-      for (int q = a.lay_ptr[l]; q < a.lay_ptr[l + 1]; ++q) {
-        const int c = a.lay_rows[q];
-        const int e0 = a.row_ptr[c], d = a.row_ptr[c + 1] - e0;
-        if (!act || d == 0) continue;
-        const uint32_t sb = a.synT[(long long)c * T + s];
-        if constexpr (ALGO == ALGO_MS) {
-          double av[DCMAX];
-          uint64_t negm = 0;
-          double min1 = __builtin_inf(), min2 = __builtin_inf();
+      // check nodes of the layer (Jacobi: all read the same posteriors), UC
+      // checks per step with every message load issued before any arithmetic
+      // (a lane walks its half-shot alone: memory-level parallelism comes
+      // from the loads in flight per step)
+      const int q1 = a.lay_ptr[l + 1];
+      for (int qb = a.lay_ptr[l]; qb < q1; qb += UC) {
+        int e0[UC], dg[UC];
+        uint32_t sb[UC];
+        double pj[UC][DCMAX];
+        Msg cj[UC][DCMAX];
+#pragma unroll
+        for (int u = 0; u < UC; ++u) {
+          const int c = qb + u < q1 ? a.lay_rows[qb + u] : 0;
+          e0[u] = a.row_ptr[c];
+          dg[u] = qb + u < q1 ? a.row_ptr[c + 1] - e0[u] : 0;
+          sb[u] = act && dg[u] ? a.synT[(long long)c * T + s] : 0u;
+          const bool l0 = ALGO == ALGO_MS && first && l == 0;   // v2c = float32(L): nothing to read
 #pragma unroll
           for (int k = 0; k < DCMAX; ++k) {
-            if (k < d) {
-              const int j = a.row_var[e0 + k], p = a.row_pos[e0 + k];
-              double v;
-              if (first && l == 0) {
-                v = (double)a.L32;                   // msg_v2c[H == 1] = L_ch, float32 (:148-149)
-              } else {
-                const bool pv = !first || !lazy || fl_var[j] < l;
-                const bool cv = !first || !lazy || fl_pos[p] < l;
-                const double pj = pv ? post[(long long)j * T + s] : L;
-                const float cj = cv ? c2v[(long long)p * T + s] : 0.0f;
-                v = pj - (double)cj;                 // v2c = post - c2v (:177)
+            pj[u][k] = L;
+            cj[u][k] = (Msg)0;
+            if (k < dg[u] && act && !l0) {
+              const int jv = a.row_var[e0[u] + k], p = a.row_pos[e0[u] + k];
+              if (!first || !lazy || fl_var[jv] < l) pj[u][k] = post[(long long)jv * T + s];
+              if (!first || !lazy || fl_pos[p] < l) cj[u][k] = c2v[(long long)p * T + s];
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < UC; ++u) {
+          const int d = dg[u];
+          if (!act || d == 0) continue;
+          if constexpr (ALGO == ALGO_MS) {
+            double av[DCMAX];
+            uint64_t negm = 0;
+            double min1 = __builtin_inf(), min2 = __builtin_inf();
+#pragma unroll
+            for (int k = 0; k < DCMAX; ++k) {
+              if (k < d) {
+                // v2c = post - c2v (:177); the first layer of the first
+                // iteration reads msg_v2c[H == 1] = L_ch as float32 (:148-149)
+                const double v = (first && l == 0) ? (double)a.L32 : pj[u][k] - (double)cj[u][k];
+                negm |= (uint64_t)(v < 0.0) << k;      // np.sign, 0 -> +1 (:157-158)
+                const double x = __builtin_fabs(v);
+                av[k] = x;
+                min2 = __builtin_fmin(min2, __builtin_fmax(min1, x));   // min of the rest (:162-164)
+                min1 = __builtin_fmin(min1, x);
               }
-              negm |= (uint64_t)(v < 0.0) << k;      // np.sign, 0 -> +1 (:157-158)
-              const double x = __builtin_fabs(v);
-              av[k] = x;
-              min2 = __builtin_fmin(min2, __builtin_fmax(min1, x));   // min of the rest (:162-164)
-              min1 = __builtin_fmin(min1, x);
             }
-          }
-          const double m1 = __builtin_isinf(min1) ? 0.0 : min1;        // (:165)
-          const double m2 = __builtin_isinf(min2) ? 0.0 : min2;        // (:166)
-          if (m1 == 0.0) fl |= FLAG_MIN_ZERO;                          // App. A.1.6 (flagged, not emulated)
-          const uint32_t negprod = (uint32_t)(__builtin_popcountll(negm) & 1) ^ sb;
-          const float c1 = (float)(a.beta * m1), c2 = (float)(a.beta * m2);   // fl32(beta * min) (:167-168)
+            const double m1 = __builtin_isinf(min1) ? 0.0 : min1;        // (:165)
+            const double m2 = __builtin_isinf(min2) ? 0.0 : min2;        // (:166)
+            if (m1 == 0.0) fl |= FLAG_MIN_ZERO;                          // App. A.1.6 (flagged, not emulated)
+            const uint32_t negprod = (uint32_t)(__builtin_popcountll(negm) & 1) ^ sb[u];
+            const float c1 = (float)(a.beta * m1), c2 = (float)(a.beta * m2);   // fl32(beta * min) (:167-168)
 #pragma unroll
-          for (int k = 0; k < DCMAX; ++k) {
-            if (k < d) {
-              const float mag = (av[k] == min1) ? c2 : c1;
-              c2v[(long long)a.row_pos[e0 + k] * T + s] = (((negm >> k) & 1u) ^ negprod) ? -mag : mag;
+            for (int k = 0; k < DCMAX; ++k) {
+              if (k < d) {
+                const float mag = (av[k] == min1) ? c2 : c1;
+                c2v[(long long)a.row_pos[e0[u] + k] * T + s] = (((negm >> k) & 1u) ^ negprod) ? -mag : mag;
+              }
             }
-          }
-        } else {
-          double th[DCMAX];
-          double prod = 1.0;
+          } else {
+            double th[DCMAX];
+            double prod = 1.0;
 #pragma unroll
-          for (int k = 0; k < DCMAX; ++k) {
-            if (k < d) {
-              const int j = a.row_var[e0 + k], p = a.row_pos[e0 + k];
-              const bool pv = !first || !lazy || fl_var[j] < l;
-              const bool cv = !first || !lazy || fl_pos[p] < l;
-              const double pj = pv ? post[(long long)j * T + s] : L;
-              const double cj = cv ? c2v[(long long)p * T + s] : 0.0;
-              th[k] = qldpc_tanh_t((pj - cj) / 2.0, lt->tanh_c);   // v2c (:269), np.tanh (:254)
-              prod *= th[k];                                        // np.prod: sequential fold
+            for (int k = 0; k < DCMAX; ++k) {
+              if (k < d) {
+                th[k] = qldpc_tanh_t((pj[u][k] - cj[u][k]) / 2.0, lt->tanh_c);   // v2c (:269), np.tanh (:254)
+                prod *= th[k];                                                  // np.prod: sequential fold
+              }
             }
-          }
 #pragma unroll
-          for (int k = 0; k < DCMAX; ++k) {
-            if (k < d) {
-              if (th[k] == 0.0) fl |= FLAG_NONFINITE;
-              double th2 = prod / th[k];                            // (:256)
-              th2 = (__builtin_fabs(th2) >= 1.0 - a.eps) ? th2 - __builtin_copysign(a.eps, th2) : th2;  // (:257-258)
-              double val = 2.0 * qldpc_atanh_t(th2, lt->atanh_hl, lt->atanh_rcp);   // (:259)
-              if (sb) val = -val;                                   // (:260-261)
-              if (!__builtin_isfinite(val)) fl |= FLAG_NONFINITE;
-              c2v[(long long)a.row_pos[e0 + k] * T + s] = val;
+            for (int k = 0; k < DCMAX; ++k) {
+              if (k < d) {
+                if (th[k] == 0.0) fl |= FLAG_NONFINITE;
+                double th2 = prod / th[k];                            // (:256)
+                th2 = (__builtin_fabs(th2) >= 1.0 - a.eps) ? th2 - __builtin_copysign(a.eps, th2) : th2;  // (:257-258)
+                double val = 2.0 * qldpc_atanh_t(th2, lt->atanh_hl, lt->atanh_rcp);   // (:259)
+                if (sb[u]) val = -val;                                // (:260-261)
+                if (!__builtin_isfinite(val)) fl |= FLAG_NONFINITE;
+                c2v[(long long)a.row_pos[e0[u] + k] * T + s] = val;
+              }
             }
           }
         }
       }
-      // variable nodes adjacent to the layer (others are unchanged, :172-177 / :265-278)
-      for (int q = a.adj_ptr[l]; q < a.adj_ptr[l + 1]; ++q) {
-        const int v = a.adj_vars[q];
-        const int p0 = a.col_ptr[v], d = a.col_ptr[v + 1] - p0;
-        if (!act) continue;
-        const long long iv = (long long)v * T + s;
-        const bool pv = !first || !lazy || fl_var[v] < l;
-        const double old = pv ? post[iv] : L;
-        double nw;
-        if constexpr (ALGO == ALGO_MS) {
-          float S = 0.0f;                                // float32, ascending check (:172)
-          for (int t = 0; t < d; ++t) {
-            const bool cv = !first || !lazy || fl_pos[p0 + t] <= l;
-            S += cv ? c2v[(long long)(p0 + t) * T + s] : 0.0f;
+      // variable nodes adjacent to the layer (others are unchanged, :172-177 /
+      // :265-278), UV variables per step, their first KV messages loaded up front
+      const int v1 = a.adj_ptr[l + 1];
+      for (int qb = a.adj_ptr[l]; qb < v1; qb += UV) {
+        int vv[UV], p0[UV], dg[UV];
+        double old[UV];
+        Msg cv[UV][KV];
+#pragma unroll
+        for (int u = 0; u < UV; ++u) {
+          vv[u] = qb + u < v1 ? a.adj_vars[qb + u] : 0;
+          p0[u] = a.col_ptr[vv[u]];
+          dg[u] = qb + u < v1 ? a.col_ptr[vv[u] + 1] - p0[u] : 0;
+          old[u] = L;
+          if (act && dg[u] && (!first || !lazy || fl_var[vv[u]] < l)) old[u] = post[(long long)vv[u] * T + s];
+#pragma unroll
+          for (int t = 0; t < KV; ++t) {
+            cv[u][t] = (Msg)0;
+            if (t < dg[u] && act && (!first || !lazy || fl_pos[p0[u] + t] <= l))
+              cv[u][t] = c2v[(long long)(p0[u] + t) * T + s];
           }
-          nw = L + (double)S;                            // (:173)
-        } else {
-          nw = d == 0 ? L : L + np_pairwise_strided(d, [&](int t) {   // (:269, :276)
-            const bool cv = !first || !lazy || fl_pos[p0 + t] <= l;
-            return cv ? c2v[(long long)(p0 + t) * T + s] : 0.0;
-          });
         }
-        post[iv] = nw;
-        if ((old < 0.0) != (nw < 0.0)) F ^= a.avar[v];   // hard decision flipped
+#pragma unroll
+        for (int u = 0; u < UV; ++u) {
+          const int d = dg[u];
+          if (!act || qb + u >= v1) continue;
+          auto get = [&](int t) -> Msg {              // message t of the column (zeros past the layer)
+            if (t < KV) return cv[u][t];
+            const bool ok = !first || !lazy || fl_pos[p0[u] + t] <= l;
+            return ok ? c2v[(long long)(p0[u] + t) * T + s] : (Msg)0;
+          };
+          double nw;
+          if constexpr (ALGO == ALGO_MS) {
+            float S = 0.0f;                              // float32, ascending check (:172)
+#pragma unroll
+            for (int t = 0; t < KV; ++t)
+              if (t < d) S += cv[u][t];
+            for (int t = KV; t < d; ++t) S += get(t);
+            nw = L + (double)S;                          // (:173)
+          } else if (d <= KV) {
+            double r = -0.0;                             // np.sum: sequential below 8 terms
+            if (d < 8) {
+#pragma unroll
+              for (int t = 0; t < KV; ++t)
+                if (t < d) r += cv[u][t];
+            } else {                                     // exactly 8: one pairwise block
+              r = ((cv[u][0] + cv[u][1]) + (cv[u][2] + cv[u][3])) + ((cv[u][4] + cv[u][5]) + (cv[u][6] + cv[u][7]));
+            }
+            nw = d == 0 ? L : L + (0.0 + r);             // (:269, :276; no edges: L0, :277-278)
+          } else {
+            nw = L + np_pairwise_strided(d, get);
+          }
+          post[(long long)vv[u] * T + s] = nw;
+          if ((old[u] < 0.0) != (nw < 0.0)) F ^= a.avar[vv[u]];   // hard decision flipped
+        }
       }
       // stop test after the layer: filters, then the exact check (:174-176)
       if (act && F == B) {
@@ -240,6 +286,7 @@ __global__ void __launch_bounds__(256) hbm_decode_kernel(HbmArgs a, const int32_
         }
         if (!un) {
           stop = true;
+          lstop = l;
           if (a.flags) a.flags[shot] = FLAG_CONVERGED | (fl & (FLAG_MIN_ZERO | FLAG_NONFINITE));
           a.iters[shot] = it + 1;
         }
@@ -252,6 +299,7 @@ __global__ void __launch_bounds__(256) hbm_decode_kernel(HbmArgs a, const int32_
         fin = true;
       } else if (it + 1 == a.max_iter) {
         fin = true;
+        lstop = a.n_layers - 1;                      // every layer ran
         if (a.flags) a.flags[shot] = fl & (FLAG_MIN_ZERO | FLAG_NONFINITE);
         a.iters[shot] = a.max_iter;
       } else {
@@ -265,8 +313,10 @@ __global__ void __launch_bounds__(256) hbm_decode_kernel(HbmArgs a, const int32_
         for (int jj = 0; jj < 64 && j0 + jj < n; ++jj) {
           if (fin) {
             const int j = j0 + jj, v = a.vinv[j];
-            // a variable no layer reaches keeps L (never written this decode)
-            const double pv = (lz && fl_var[v] >= a.n_layers) ? L : post[(long long)v * T + s];
+            // a variable no layer has reached yet keeps L (never written in
+            // this decode: no layer adjacent to it, or a first-iteration stop)
+            const bool unwritten = lz && (fl_var[v] >= a.n_layers || (it == 0 && fl_var[v] > lstop));
+            const double pv = unwritten ? L : post[(long long)v * T + s];
             const bool bit = pv < 0.0;                   // (:174 / :280)
             if (a.eh_bits) w |= (uint64_t)bit << jj;
             else a.ehat[shot * (long long)n + j] = (uint8_t)bit;
