@@ -66,8 +66,8 @@ const char *qldpc_version(void);
 int qldpc_device_count(void);
 
 /* Build the Tanner graph of H (row-major uint8 m x n, entries taken mod 2,
- * as load_matrix's `(mat % 2)`, simulator.py:35) and upload it to the current
- * device. Replaces the per-call `np.where(H)` edge construction of
+ * as load_matrix's `(mat % 2)`, simulator.py:35; any size) and upload it to
+ * the current device. Replaces the per-call `np.where(H)` edge construction of
  * BP_decoder (decoders.py:224-229) and MS_decoder's dense H masks
  * (decoders.py:148-169). */
 int qldpc_code_create(const uint8_t *h_H, int m, int n, qldpc_code **out);
@@ -95,7 +95,11 @@ int qldpc_schedule_destroy(qldpc_schedule *sched);
  *   d_ehat  uint8 [batch][n]   hard decisions, original column order
  *   d_iters int32 [batch]      iterations as returned by the reference
  *   d_post  double[batch][n]   final posterior LLRs (nullable)
- *   d_flags int32 [batch]      QLDPC_FLAG_* (nullable) */
+ *   d_flags int32 [batch]      QLDPC_FLAG_* (nullable)
+ * Any size of H decodes: codes whose per-half-shot state fits a CU's LDS
+ * (and whose tables fit 16 bits) run the LDS-resident kernels, others the
+ * HBM-resident kernel (row degree <= 64), with identical results. The
+ * prior L = log((1-p)/max(p, eps)) is NumPy's log (decoders.py:147, :232). */
 int qldpc_decode_device(const qldpc_code *code, const qldpc_schedule *sched, int algo,
                         const uint8_t *d_syn, int64_t batch, double p, int max_iter, double beta,
                         double eps, uint8_t *d_ehat, int32_t *d_iters, double *d_post,

@@ -90,8 +90,9 @@ __device__ __forceinline__ double qldpc_div_dev(double a, double b) {
 #define QLDPC_DIV(a, b) ((a) / (b))
 #endif
 
-/* the table image: NumPy's tanh intervals [16][18] (b, c0 .. c16), SVML
-   atanh's log(1 + i/16) [16][2] (hi, lo) and its reciprocal step buckets */
+/* the table image: NumPy's tanh intervals (rows b, c0 .. c16 as [9][16][2]
+   row pairs), SVML atanh's log(1 + i/16) [16][2] (hi, lo) and its
+   reciprocal step buckets */
 typedef struct {
   double tanh_c[16 * 18];
   double atanh_hl[16 * 2];
@@ -107,25 +108,27 @@ QLDPC_HD double qldpc_tanh_t(double x, const double* tc) {
   int32_t h = (int32_t)(uint32_t)(nd >> 32) - 0x3fc00000;
   h = h < 0 ? 0 : h;
   h = h > 0x780000 ? 0x780000 : h;
-  const double* c = tc + 18 * (h >> 19);              /* interval 0 .. 15 */
-  const double y = qldpc_bits2d(u & 0x7fffffffffffffffull) - c[0];
-  double r = c[17];
-  r = QLDPC_FMA(r, y, c[16]);
-  r = QLDPC_FMA(r, y, c[15]);
-  r = QLDPC_FMA(r, y, c[14]);
-  r = QLDPC_FMA(r, y, c[13]);
-  r = QLDPC_FMA(r, y, c[12]);
-  r = QLDPC_FMA(r, y, c[11]);
-  r = QLDPC_FMA(r, y, c[10]);
-  r = QLDPC_FMA(r, y, c[9]);
-  r = QLDPC_FMA(r, y, c[8]);
-  r = QLDPC_FMA(r, y, c[7]);
-  r = QLDPC_FMA(r, y, c[6]);
-  r = QLDPC_FMA(r, y, c[5]);
-  r = QLDPC_FMA(r, y, c[4]);
-  r = QLDPC_FMA(r, y, c[3]);
-  r = QLDPC_FMA(r, y, c[2]);
-  r = QLDPC_FMA(r, y, c[1]);
+  const double* c = tc + 2 * (h >> 19);               /* interval 0 .. 15; row k at c[32 (k/2) + k%2] */
+#define QLDPC_TC(k) c[32 * ((k) / 2) + ((k) & 1)]
+  const double y = qldpc_bits2d(u & 0x7fffffffffffffffull) - QLDPC_TC(0);
+  double r = QLDPC_TC(17);
+  r = QLDPC_FMA(r, y, QLDPC_TC(16));
+  r = QLDPC_FMA(r, y, QLDPC_TC(15));
+  r = QLDPC_FMA(r, y, QLDPC_TC(14));
+  r = QLDPC_FMA(r, y, QLDPC_TC(13));
+  r = QLDPC_FMA(r, y, QLDPC_TC(12));
+  r = QLDPC_FMA(r, y, QLDPC_TC(11));
+  r = QLDPC_FMA(r, y, QLDPC_TC(10));
+  r = QLDPC_FMA(r, y, QLDPC_TC(9));
+  r = QLDPC_FMA(r, y, QLDPC_TC(8));
+  r = QLDPC_FMA(r, y, QLDPC_TC(7));
+  r = QLDPC_FMA(r, y, QLDPC_TC(6));
+  r = QLDPC_FMA(r, y, QLDPC_TC(5));
+  r = QLDPC_FMA(r, y, QLDPC_TC(4));
+  r = QLDPC_FMA(r, y, QLDPC_TC(3));
+  r = QLDPC_FMA(r, y, QLDPC_TC(2));
+  r = QLDPC_FMA(r, y, QLDPC_TC(1));
+#undef QLDPC_TC
   r = nd <= 0x7fe0000000000000ull ? r : 1.0;         /* |x| >= 2^1023, inf */
   r = qldpc_bits2d(qldpc_d2bits(r) | (u & 0x8000000000000000ull));
   return (x == x) ? r : qldpc_bits2d(0x7ff8000000000000ull);

@@ -156,15 +156,18 @@ def main():
         buckets.append(below | (thr << 8))
     L = []
     L.append("/* Generated by tools/gen_numpy_libm_tables.py from NumPy %s (%s): DO NOT EDIT." % (numpy.__version__, os.path.basename(so)))
-    L.append(" * tanh:   NumPy simd_tanh_f64 lut16x18 (loops_hyperbolic.dispatch.c.src), stored [interval][18].")
+    L.append(" * tanh:   NumPy simd_tanh_f64 lut16x18 (loops_hyperbolic.dispatch.c.src), stored as [9][16][2] row pairs.")
     L.append(" * atanh:  __svml_atanh8_ha data (__svml_datanh_ha_data_internal_avx512).")
     L.append(" * log:    __svml_log8_ha data (__svml_dlog_ha_data_internal_avx512).")
     L.append(" * rcp:    mantissa thresholds of the rounded vrcp14pd step functions (probed on the capture host). */")
     L.append("#ifndef QLDPC_NUMPY_TABLES_H\n#define QLDPC_NUMPY_TABLES_H\n")
-    L.append("/* [16][18]: b, c0 .. c16 of interval i (tanh(|x|) = sum c_k (|x| - b)^k) */")
+    L.append("/* [9][16][2]: row pair (2q, 2q+1) of interval i, rows = b, c0 .. c16 of")
+    L.append("   tanh(|x|) = sum c_k (|x| - b)^k. Pair-major: one 16-byte read fetches two")
+    L.append("   rows of a lane's interval, and 16 lanes' reads of a pair fall in one 256-byte")
+    L.append("   block (distinct LDS banks whatever the intervals). */")
     L.append("#define QLDPC_TANH_LUT_INIT { \\")
-    for i in range(16):
-        L.append("  " + ", ".join(hexd(tanh[r][i]) for r in range(18)) + ", \\")
+    for q in range(9):
+        L.append("  " + ", ".join(f"{hexd(tanh[2 * q][i])}, {hexd(tanh[2 * q + 1][i])}" for i in range(16)) + ", \\")
     L.append("}")
     L.append("/* [16][2]: log(1 + i/16) as hi + lo (atanh) */")
     L.append("#define QLDPC_ATANH_HL_INIT { \\")
