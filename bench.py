@@ -436,12 +436,16 @@ def roofline(names, t_launch, hs_launch, it_launch, algo_launch, launches):
                      "(tools/gpu_profile_roofline.sh regenerates it): bound and frac unmeasured")
         return r
     pu = prof["per_half_shot_iteration"]
+    valu_lo = None
     if "valu_cycles" in pu:
         # VALU issue time by instruction class (32-bit ops 2 cycles per wave64
-        # on a SIMD-32, float64 add/mul/fma 4, transcendentals 8/16), per SIMD
-        valu = pu["valu_cycles"] * it_launch / t_launch / 1e9            # G SIMD-cycles / s
+        # on a SIMD-32, float64 add/mul/fma 4, transcendentals 8/16), per SIMD;
+        # the unclassified remainder (float64 min/max/compare among them) at
+        # the float64 rate: an upper bound, the lower one beside it
+        valu = pu.get("valu_cycles_hi", pu["valu_cycles"]) * it_launch / t_launch / 1e9   # G SIMD-cycles / s
+        valu_lo = pu["valu_cycles"] * it_launch / t_launch / 1e9
         valu_peak = SIMDS * CLOCK_GHZ
-        valu_unit = "G SIMD VALU-issue cycles/s (class-weighted)"
+        valu_unit = "G SIMD VALU-issue cycles/s (class-weighted, upper bound)"
     else:
         valu = pu["valu_insts"] * it_launch / t_launch / 1e9             # G wave-instructions / s
         valu_peak = SIMDS * CLOCK_GHZ / VALU_CYCLES
@@ -450,7 +454,8 @@ def roofline(names, t_launch, hs_launch, it_launch, algo_launch, launches):
     lds_peak = CUS * CLOCK_GHZ
     traffic = prof["per_half_shot"]["hbm_bytes"] * hs_launch
     units = {"valu": {"achieved": valu, "peak": valu_peak, "unit": valu_unit,
-                      "frac": valu / valu_peak},
+                      "frac": valu / valu_peak,
+                      "frac_lo": None if valu_lo is None else valu_lo / valu_peak},
              "lds": {"achieved": lds, "peak": lds_peak, "unit": "G LDS-array cycles/s (all CUs)",
                      "frac": lds / lds_peak}}
     bound = max(units, key=lambda k: units[k]["frac"])
@@ -459,7 +464,8 @@ def roofline(names, t_launch, hs_launch, it_launch, algo_launch, launches):
     r["hbm"].update(achieved_gbs=traffic / t_launch / 1e9, frac=traffic / t_launch / 1e9 / HBM_PEAK_GBS)
     r["formula"] = ("valu frac = valu_cycles/half-shot-iter x iterations/launch / (1024 SIMDs x 2.4 GHz x "
                     "launch time), valu_cycles = 2 x SQ_INSTS_VALU + 2 x (ADD+MUL+FMA_F64) + 14 x TRANS_F64 + "
-                    "6 x TRANS_F32 (per-class SQ_INSTS_VALU_* counters); lds frac = lds_cycles/half-shot-iter x "
+                    "6 x TRANS_F32 (per-class SQ_INSTS_VALU_* counters) + 2 x the unclassified rest "
+                    "(float64 min/max/compare have no class counter; frac_lo leaves it out); lds frac = lds_cycles/half-shot-iter x "
                     "iterations/launch / (256 CUs x 2.4 GHz x launch time); per-unit counts from the "
                     "profile (SQ_INSTS_VALU, SQ_LDS_IDX_ACTIVE; traffic = 2 x FETCH_SIZE + WRITE_SIZE), "
                     "launch time and iterations from this run")

@@ -112,6 +112,11 @@ def summarise_config(d):
             ent["per_half_shot_iteration"]["valu_classes"] = pc
             ent["per_half_shot_iteration"]["valu_cycles"] = (2 * tot + 2 * f64 + 14 * pc["trans_f64"] +
                                                               6 * pc["trans_f32"])
+            # the unclassified remainder holds float64 min / max / compares
+            # (v_min_f64 & co. have no class counter): upper bound = all of it
+            # at the float64 rate
+            ent["per_half_shot_iteration"]["valu_cycles_hi"] = \
+                ent["per_half_shot_iteration"]["valu_cycles"] + 2 * max(pc["other"], 0.0)
         # the SQ pass's own dispatches: busy fractions at its measured clock
         v, hs, it = c["GRBM_GUI_ACTIVE"]
         cyc = v / 8.0
