@@ -7,7 +7,7 @@
 #define QLDPC_MAX_THREADS 768
 // max runs of equal column degree the flooding MS kernel handles
 #define QLDPC_MAX_RUNS 8
-#define QLDPC_FLOOD_HDR 128  // LDS bytes of ms_flood_kernel's runs header (4 * 8 ints)
+#define QLDPC_FLOOD_HDR 160  // LDS bytes of ms_flood_kernel's runs header (5 * 8 ints)
 
 namespace qldpc {
 

@@ -860,9 +860,15 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) decode_kernel(DecodeArgs a)
 //    addressing. Pad checks (c >= m) read post[0] and write the 8-float pad
 //    behind c2v; `livem` masks their flags.
 //  * Variable nodes are visited by runs of equal column degree K (variables
-//    are relabeled by degree, so the CSC start of variable start + o is
-//    p0 + o * K): no per-variable table, no masking, a compile-time K.
-// The LDS then holds only wave state: post f64[n] | c2v f32[E + 8].
+//    are relabeled by degree): no per-variable table, no masking, a
+//    compile-time K. Message t of variable start + o sits at p0 + o * K + t
+//    (stride 0: the CSC order) or, in the bank-conflict-free layout of
+//    quasi-cyclic lift-16 codes (capi.cpp flood_qc16_layout),
+//    at p0 + t * stride + o.
+//  * Lane / slot i of the wave owns check chk[lane + 64 i] (-1 = pad): the
+//    QC layout pairs block rows so that every LDS access of the check node is
+//    conflict-free, which fixes which lanes hold which checks.
+// The LDS then holds only wave state: post f64[labels] | c2v f32[slots].
 // ---------------------------------------------------------------------------
 // Per-lane edge addresses of the KC checks a lane owns: absolute LDS byte
 // addresses, 16 VGPRs per check, no VALU per use.
@@ -895,6 +901,8 @@ struct FloodTab {
 struct FloodRuns {  // fblob header: runs of equal column degree (capi.cpp)
   int n_runs;
   int start[QLDPC_MAX_RUNS], count[QLDPC_MAX_RUNS], deg[QLDPC_MAX_RUNS], p0[QLDPC_MAX_RUNS];
+  int stride[QLDPC_MAX_RUNS];  // 0: message t of variable o at p0 + o K + t; else p0 + t stride + o
+  int off_chk;                 // fblob byte offset of int16 chk[8 * 64]: check of (lane, slot), -1 = pad
 };
 
 // Sequential float32 sum in ascending check order (np.sum axis=0). It starts
@@ -937,6 +945,29 @@ __device__ __forceinline__ void vn_run(const DecodeArgs& a, double* post, const 
   if (o0 + lane < count) po[o0] = a.L + (double)vn_sum<K>(c + o0 * K);
 }
 
+// slot-major run: message t of variable start + o at p0 + t * S + o (S a
+// multiple of 32): each read of a 64-variable chunk is 64 consecutive floats
+template <int K>
+__device__ __forceinline__ void vn_run_sm(const DecodeArgs& a, double* post, const float* c2v,
+                                          int start, int count, int p0, int S, int lane) {
+  const float* c = c2v + p0 + lane;
+  double* po = post + start + lane;
+  auto sum = [&](int o0) {
+    float s = c[o0];
+#pragma unroll
+    for (int t = 1; t < K; ++t) s += c[o0 + t * S];     // float32, ascending check
+    return s;
+  };
+  int o0 = 0;
+  for (; o0 + 128 <= count; o0 += 128) {
+    const float s0 = sum(o0), s1 = sum(o0 + 64);
+    po[o0] = a.L + (double)s0;
+    po[o0 + 64] = a.L + (double)s1;
+  }
+  for (; o0 + 64 <= count; o0 += 64) po[o0] = a.L + (double)sum(o0);
+  if (o0 + lane < count) po[o0] = a.L + (double)sum(o0);
+}
+
 __device__ __forceinline__ void vn_run_any(const DecodeArgs& a, double* post, const float* c2v,
                                            int start, int count, int K, int p0, int lane) {
   for (int o = lane; o < count; o += 64) {
@@ -969,19 +1000,23 @@ ms_flood_kernel(DecodeArgs a) {
   double* post = (double*)ws;
   unsigned char* c2v_b = ws + a.off_c2v;
   const float* c2v_f = (const float*)c2v_b;
-  const int m = a.m, n = a.n;
+  const int n = a.n;
 
   // static per-lane graph data (VGPRs for the kernel)
   FloodTab<KC> tab;
   tab.init(ftab, lane, lds_addr(ws), lds_addr(ws) + (uint32_t)a.off_c2v);
+  const int16_t* chk = (const int16_t*)(a.blob + __builtin_amdgcn_readfirstlane(runs->off_chk));
+  int lchk[KC];
   uint32_t livem = 0;
 #pragma unroll
-  for (int i = 0; i < KC; ++i)
-    if (lane + 64 * i < m) livem |= 1u << i;
+  for (int i = 0; i < KC; ++i) {
+    lchk[i] = chk[lane + 64 * i];
+    if (lchk[i] >= 0) livem |= 1u << i;
+  }
   // the runs header lives in LDS (the first QLDPC_FLOOD_HDR bytes): one
   // broadcast read per field per iteration, no global latency in the loop
   const int n_runs = __builtin_amdgcn_readfirstlane(runs->n_runs);
-  if (threadIdx.x < 4 * QLDPC_MAX_RUNS) ((int*)lds)[threadIdx.x] = (&runs->start[0])[threadIdx.x];
+  if (threadIdx.x < 5 * QLDPC_MAX_RUNS) ((int*)lds)[threadIdx.x] = (&runs->start[0])[threadIdx.x];
   __syncthreads();
   const int* hdr = (const int*)lds;
 
@@ -993,10 +1028,8 @@ ms_flood_kernel(DecodeArgs a) {
     bool conv = false;
     uint32_t synreg = 0;
 #pragma unroll
-    for (int i = 0; i < KC; ++i) {
-      const int c = lane + 64 * i;
-      if (c < m) synreg |= syn_bit(a, hs, c) << i;
-    }
+    for (int i = 0; i < KC; ++i)
+      if (lchk[i] >= 0) synreg |= syn_bit(a, hs, lchk[i]) << i;
     for (int it = 0;; ++it) {
       uint32_t unsat = 0;
       if (it == 0) {
@@ -1036,6 +1069,25 @@ ms_flood_kernel(DecodeArgs a) {
         const int cnt = __builtin_amdgcn_readfirstlane(hdr[QLDPC_MAX_RUNS + r]);
         const int K = __builtin_amdgcn_readfirstlane(hdr[2 * QLDPC_MAX_RUNS + r]);
         const int p0 = __builtin_amdgcn_readfirstlane(hdr[3 * QLDPC_MAX_RUNS + r]);
+        const int S = __builtin_amdgcn_readfirstlane(hdr[4 * QLDPC_MAX_RUNS + r]);
+        if (S) {
+          switch (K) {
+            case 0: vn_run<0>(a, post, c2v_f, st, cnt, p0, lane); break;
+            case 1: vn_run<1>(a, post, c2v_f, st, cnt, p0, lane); break;
+            case 2: vn_run_sm<2>(a, post, c2v_f, st, cnt, p0, S, lane); break;
+            case 3: vn_run_sm<3>(a, post, c2v_f, st, cnt, p0, S, lane); break;
+            case 4: vn_run_sm<4>(a, post, c2v_f, st, cnt, p0, S, lane); break;
+            case 5: vn_run_sm<5>(a, post, c2v_f, st, cnt, p0, S, lane); break;
+            case 6: vn_run_sm<6>(a, post, c2v_f, st, cnt, p0, S, lane); break;
+            default:
+              for (int o = lane; o < cnt; o += 64) {
+                float sv = 0.0f;
+                for (int t = 0; t < K; ++t) sv += c2v_f[p0 + t * S + o];
+                post[st + o] = a.L + (double)sv;
+              }
+          }
+          continue;
+        }
         switch (K) {
           case 0: vn_run<0>(a, post, c2v_f, st, cnt, p0, lane); break;
           case 1: vn_run<1>(a, post, c2v_f, st, cnt, p0, lane); break;
