@@ -269,6 +269,7 @@ struct LaunchCfg {
   bool lblob = false;  // uses the layer-ordered blob (ms_layered_kernel)
   bool gtab = false;     // ms_flood_kernel: global tables, LDS = wave state only
   bool tlg = false;      // bp_team_lg_kernel: every table global, LDS image = layer pointers
+  bool cc = false;       // ms_layered_cc_kernel: compressed check records
   int team = 0;          // bp_team_kernel: waves per half-shot (one workgroup), 0 = wave kernels
   const char* name = "";  // kernel name as rocprofv3 reports it
   bool ok = false;
@@ -285,7 +286,7 @@ struct qldpc_schedule {
   std::vector<uint8_t> lblob;
   unsigned char* d_lblob = nullptr;
   int l_off_ltab = 0, l_off_lrow = 0, l_off_lay_ptr = 0, l_off_adj_ptr = 0, l_off_adj_vars = 0,
-      l_off_adj_info = 0, l_off_adj_dmax = 0, l_off_vn_chk = 0;
+      l_off_adj_info = 0, l_off_adj_dmax = 0, l_off_vn_chk = 0, l_off_vn_ck = 0;
   int off_cn_tab = 0, off_row_ptr = 0, off_vn_ptr = 0, off_vn_chk = 0;
   int off_lay_ptr = 0, off_lay_rows = 0, off_adj_ptr = 0, off_adj_vars = 0, off_chunk_dmax = 0;
   unsigned char* d_blob = nullptr;
@@ -750,6 +751,15 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
       s->l_off_adj_info = put(s->lblob, adj_info);
       s->l_off_adj_dmax = put(s->lblob, adj_dmax);
       s->l_off_vn_chk = put(s->lblob, code->avar);   // filter word per relabeled variable
+      if (16 * m < 65536) {
+        // ms_layered_cc_kernel: per CSC position 16 * check + edge index (its
+        // record and message), 8 pad entries for the unrolled VN reads
+        std::vector<uint16_t> vn_ck(code->E + 8, 0);
+        for (int r = 0; r < m; ++r)
+          for (int e = code->row_ptr[r]; e < code->row_ptr[r + 1]; ++e)
+            vn_ck[code->edge_pos[e]] = (uint16_t)(16 * r + (e - code->row_ptr[r]));
+        s->l_off_vn_ck = put(s->lblob, vn_ck);
+      }
       s->lblob.resize(align16((int)s->lblob.size() + 1));
     }
   }
@@ -871,6 +881,13 @@ static void flood_wave_layout(const qldpc_schedule* s, int* bytes, int* off_c2v)
   *bytes = align16(*off_c2v + 4 * s->f_n_c2v);
 }
 
+// ms_layered_cc_kernel's slice: column sums f32[n] | records uint4[m] | syn words
+static void cc_wave_layout(const qldpc_code* c, int* bytes, int* off_rec, int* off_synw) {
+  *off_rec = align16(4 * c->n);
+  *off_synw = align16(*off_rec + 16 * c->m);
+  *bytes = align16(*off_synw + 4 * 2 * ((c->m + 63) / 64));
+}
+
 static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   std::lock_guard<std::mutex> lk(s->mu);
   LaunchCfg& cfg = s->cfg[algo];
@@ -899,7 +916,12 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
     if (const char* ev = getenv("QLDPC_MS_LANES_PER_CHECK")) g = atoi(ev);
     // (several half-shots per wave, ms_layered_grp_kernel, measured 2x slower
     // in round 2: at a fixed LDS budget it halves the waves per CU; removed)
-    cfg.kernel = qldpc::select_ms_layered_kernel(dc, g, &cfg.name);
+    if (g == 1 && s->l_off_vn_ck > 0 && !getenv("QLDPC_MS_C2V_FULL")) {
+      cfg.kernel = qldpc::select_ms_layered_cc_kernel(dc, &cfg.name);
+      cfg.cc = cfg.kernel != nullptr;
+      if (cfg.cc) max_waves = 16;
+    }
+    if (!cfg.kernel) cfg.kernel = qldpc::select_ms_layered_kernel(dc, g, &cfg.name);
     use_lblob = cfg.kernel != nullptr;
   }
   cfg.lblob = use_lblob;
@@ -935,6 +957,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   wave_layout(c, s->layered, algo, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw, use_lblob);
   if (team) team_layout(c, team, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw, &off_red);
   if (gtab) flood_wave_layout(s, &cfg.wave_bytes, &off_c2v);
+  if (cfg.cc) cc_wave_layout(c, &cfg.wave_bytes, &off_c2v, &off_synw);
   int max_lds = 0, dev = 0;
   HIP_TRY(hipGetDevice(&dev));
   HIP_TRY(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
@@ -1219,6 +1242,10 @@ extern "C" int qldpc_decode_device_ex(const qldpc_code* code, const qldpc_schedu
     a.off_row_ptr = sched->l_off_adj_info;
     a.off_chunk_dmax = sched->l_off_adj_dmax;
     a.off_vn_chk = sched->l_off_vn_chk;
+    if (cfg->cc) {
+      a.off_vn_ptr = sched->l_off_vn_ck;
+      cc_wave_layout(code, &a.wave_bytes, &a.off_c2v, &a.off_synw);
+    }
   }
   if (cfg->team) team_layout(code, cfg->team, &a.wave_bytes, &a.off_c2v, &a.off_synw, &a.off_parw, &a.off_red);
   if (cfg->tlg) {  // bp_team_lg_kernel: layer pointers in LDS, every table global
@@ -1748,7 +1775,7 @@ static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t*
   const int mr = rt * bblk;                          // its row slots
   const int base = align16(4 * n + 4 * (m + 2) + n) + (order == 1 ? 4 * setdiff_table_ints(n) : 0);
   const int lds_col = base + 8 * nw * (1 + 2 * 16 + 2) + 4 * 32 + 16;         // emask, candidate / xrow rows, slots, misc
-  const int lds_blk = base + 8 * nw * (1 + 64) + 8 * 64 + 8 * 2 * mr + 4 * 3 * mr + 4 * 64 + 32;
+  const int lds_blk = base + 8 * nw * (1 + 64) + 8 * 64 + 8 * 2 * mr + 4 * 3 * mr + 4 * 64 + 64;
                       // emask, PW, CT, Wd / Cm, pkof / pidx / crow, pk, misc
   int dev = 0, max_lds = 0;
   HIP_TRY(hipGetDevice(&dev));
@@ -1782,6 +1809,18 @@ static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t*
     HIP_TRY(hipMemset(d_prof, 0, 16 * sizeof(unsigned long long)));
   }
   a.prof = d_prof;
+  {
+    // per-CU workgroup tickets of osd_block_kernel (engine SIMD choice), one
+    // zeroed array per device; the counters only ever wrap
+    static std::mutex mu;
+    static uint32_t* tickets[64] = {};
+    std::lock_guard<std::mutex> lk(mu);
+    if (dev >= 0 && dev < 64 && !tickets[dev] && !getenv("QLDPC_OSD_NO_TICKETS")) {
+      HIP_TRY(hipMalloc(&tickets[dev], sizeof(uint32_t) * qldpc::kOsdCuSlots));
+      HIP_TRY(hipMemset(tickets[dev], 0, sizeof(uint32_t) * qldpc::kOsdCuSlots));
+    }
+    a.cu_tickets = (dev >= 0 && dev < 64 && !getenv("QLDPC_OSD_NO_TICKETS")) ? tickets[dev] : nullptr;
+  }
   int64_t done = 0;
   while (done < count) {  // grid.x limit
     const int64_t g = std::min<int64_t>(count - done, 1 << 30);

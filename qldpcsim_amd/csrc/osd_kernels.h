@@ -28,6 +28,7 @@ struct OsdArgs {
   int32_t* spill_count;    // [1]
   long long spill_cap, shot_base;
   unsigned long long* prof; // QLDPC_OSD_TIMING builds only: per-phase cycle sums
+  uint32_t* cu_tickets;    // [kOsdCuSlots] per-CU workgroup tickets (engine SIMD choice), or null
   int redo;                // osd_kernel only: process just the shots whose status is 3
                            // (left by osd_block_kernel: syndrome outside H's column space)
 };
@@ -44,6 +45,7 @@ struct OrderArgs {
   int n, np2;              // np2 = power of two >= n (<= 2048)
 };
 constexpr int kOrderMarginUlp = 64;
+constexpr int kOsdCuSlots = 16 * 256;  // XCC id (4 bits) x HW_ID bits 8-15 (CU, SH, SE)
 hipError_t launch_osd_order(const OrderArgs& a, long long count, hipStream_t stream);
 
 const void* select_osd_kernel(int nw);  // nw = 64-bit words per row incl. the syndrome column

@@ -66,6 +66,10 @@ __device__ __forceinline__ void spill_shot(const OsdArgs& a, long long shot, int
 #define QLDPC_ABLATE_OSD 0  // timing-only builds of osd_block_kernel: bit 0 skips phase D, bit 1 the engine
 #endif
 
+// s_getreg immediates: (size - 1) << 11 | offset << 6 | register id
+constexpr int kHwRegHwId = (31 << 11) | 4;    // HW_ID: SIMD bits 4-5, CU 8-11, SH 12, SE 13-15
+constexpr int kHwRegXccId = (31 << 11) | 20;  // XCC_ID: bits 0-3
+
 template <int NW>
 __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
   // LDS: inv_perm[n] | J list [m+2] | inJ bytes [n] | emask [NW] u64 |
@@ -418,7 +422,9 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
   int* crow = pidx + MR;                             // compact position -> row (free rows)
   int* pk = crow + MR;                               // pivot k: compact position << 6 | column bit
   int* misc = pk + 64;                               // [0] nJ [1] rank [2] i0 [3] flag [4] done [5] K
-  int* table = misc + 8;                             // [6..7] this block's pivot-column mask
+                                                     // [6..7] this block's pivot-column mask
+                                                     // [8..11] SIMD of each wave [12] engine SIMD
+  int* table = misc + 16;
 
   const int t = threadIdx.x;
   // readfirstlane: `wave` is then known to be wave-uniform, so the engine's
@@ -438,8 +444,30 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
     pkof[t + h * B] = -1;
     pidx[t + h * B] = m;
   }
-  if (t == 0) misc[3] = 0;
+  // Phase B runs on one "engine" wave while the workgroup's other waves wait
+  // at the barrier, and a CU runs 4 shots (workgroups) whose 4 waves sit on
+  // its 4 SIMDs, wave 0 on a SIMD that rotates between workgroups: engines of
+  // co-resident shots often shared a SIMD. Each workgroup takes a per-CU
+  // ticket and runs its engine on the wave placed on SIMD (ticket mod 4), so
+  // the engines of 4 consecutive workgroups of a CU use 4 SIMDs.
+  if (lane == 0 && wave < 4) misc[8 + wave] = (int)((__builtin_amdgcn_s_getreg(kHwRegHwId) >> 4) & 3u);
+  if (t == 0) {
+    misc[3] = 0;
+    uint32_t tk = 0;
+    if (a.cu_tickets) {
+      const uint32_t hw = __builtin_amdgcn_s_getreg(kHwRegHwId), xcc = __builtin_amdgcn_s_getreg(kHwRegXccId);
+      tk = atomicAdd(a.cu_tickets + (((xcc & 15u) << 8) | ((hw >> 8) & 0xffu)), 1u);
+    }
+    misc[12] = (int)(tk & 3u);
+  }
   __syncthreads();
+  int engine = 0;
+  {
+    const int target = misc[12], nwv = (int)(blockDim.x >> 6);
+    for (int w = 0; w < 4 && w < nwv; ++w)
+      if (misc[8 + w] == target) engine = w;
+    engine = __builtin_amdgcn_readfirstlane(engine);
+  }
 
   // my rows of Hp (+ syndrome bit at column n)
   uint64_t R[RT][NW];
@@ -495,7 +523,7 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
       }
     __syncthreads();
     QLDPC_TICK(1);
-    if (wave == 0) {                                  // B
+    if (wave == engine) {                             // B
       // the engine works on the rows still free (no pivot yet), compacted:
       // crow[c] = the c-th free row; earlier pivots are reduced in phase D
       const int rank0 = rank;

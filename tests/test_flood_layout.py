@@ -128,6 +128,8 @@ def test_gpu_qc_layout_equals_plain_layout(monkeypatch):
         for plain in (False, True):
             if plain:
                 monkeypatch.setenv("QLDPC_FLOOD_PLAIN", "1")
+            else:
+                monkeypatch.delenv("QLDPC_FLOOD_PLAIN", raising=False)
             monkeypatch.setattr(_lib, "_code_cache", {})   # a fresh code + schedule under the env
             monkeypatch.setattr(_lib, "_code_fast", {})
             m = H.shape[0]
