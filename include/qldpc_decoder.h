@@ -112,17 +112,6 @@ int qldpc_decode_device(const qldpc_code *code, const qldpc_schedule *sched, int
 int qldpc_decode_kernel_name(const qldpc_code *code, const qldpc_schedule *sched, int algo,
                              char *buf, int len);
 
-/* Table image of ms_flood_kernel (flooding min-sum, uniform row degree): the
- * int32 header n_runs, start[8], count[8], deg[8], p0[8], stride[8], off_chk;
- * the uint32 edge words ((4 * message slot) << 16 | 8 * post label, 8 per
- * check) at *off_tab for check slots lane + 64 * slot; int16 check per slot
- * (-1 = pad) at off_chk; uint16 post label per column at *off_label.
- * *qc_layout = 1 for the bank-conflict-free lift-16 layout. *image = NULL
- * when the schedule has no such image. Host memory owned by the schedule.
- * No reference counterpart (layout inspection for tests). */
-int qldpc_schedule_flood_image(const qldpc_schedule *sched, const uint8_t **image, int *bytes, int *off_tab,
-                               int *off_label, int *qc_layout);
-
 /* qldpc_decode_device with a choice of formats: d_syn uint8 [batch][m]
  * (QLDPC_FMT_BYTES) or uint64 [batch][ceil(m/64)] (QLDPC_FMT_BITS); d_ehat
  * uint8 [batch][n] or uint64 [batch][ceil(n/64)]. Bit-packed I/O cuts the

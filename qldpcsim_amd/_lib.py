@@ -24,7 +24,7 @@ EXPORTS = (
     "qldpc_code_create", "qldpc_code_destroy", "qldpc_code_shape",
     "qldpc_schedule_create", "qldpc_schedule_destroy",
     "qldpc_decode_device", "qldpc_decode_device_ex", "qldpc_decode_host", "qldpc_decode_kernel_name",
-    "qldpc_schedule_flood_image", "qldpc_osd_decode", "qldpc_osd_decode_batch", "qldpc_osd_device", "qldpc_osd_order_device",
+    "qldpc_osd_decode", "qldpc_osd_decode_batch", "qldpc_osd_device", "qldpc_osd_order_device",
     "qldpc_osd_device_ordered", "qldpc_osd_device_ordered_ex", "qldpc_cpython_setdiff_first",
     "qldpc_channel_thresholds", "qldpc_channel_sample", "qldpc_channel_sample_ex", "qldpc_count_outcomes",
     "qldpc_count_outcomes_ex",
@@ -66,7 +66,6 @@ def _load():
         "qldpc_decode_device_ex": ([P, P, I, P, I, I64, D, I, D, D, P, I, P, P, P, P], I),
         "qldpc_decode_host": ([P, P, I, P, I64, D, I, D, D, P, P, P, P], I),
         "qldpc_decode_kernel_name": ([P, P, I, ctypes.c_char_p, I], I),
-        "qldpc_schedule_flood_image": ([P, PP, P, P, P, P], I),
         "qldpc_osd_decode": ([P, P, P, I, P, P, P, I], I),
         "qldpc_osd_decode_batch": ([P, I64, P, P, I, P, I], I),
         "qldpc_osd_device": ([P, I64, P, P, I, P, P, P], I),
@@ -211,28 +210,6 @@ def kernel_name(H, layer_ptr, layer_rows, algo, device_index=None):
     buf = ctypes.create_string_buffer(128)
     check(lib.qldpc_decode_kernel_name(code.handle, sched.handle, ALGO[algo], buf, 128))
     return buf.value.decode()
-
-
-def flood_image(H, layer_ptr, layer_rows, device_index=None):
-    """ms_flood_kernel's table image of a flooding schedule (None if it has
-    none): dict of the runs header, edge words [8 * 64][8], check per slot,
-    post label per column, and whether the lift-16 bank layout was used."""
-    code = code_for(H, device_index)
-    sched = code.schedule(layer_ptr, layer_rows)
-    img, nb, ot, ol, qc = ctypes.c_void_p(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-    check(lib.qldpc_schedule_flood_image(sched.handle, ctypes.byref(img), ctypes.byref(nb), ctypes.byref(ot),
-                                         ctypes.byref(ol), ctypes.byref(qc)))
-    if not img.value:
-        return None
-    raw = np.frombuffer(ctypes.string_at(img.value, nb.value), np.uint8)
-    R = 8
-    hdr = raw[:4 * (2 + 5 * R)].view(np.int32)
-    oc = int(hdr[1 + 5 * R])
-    return {"n_runs": int(hdr[0]), "start": hdr[1:1 + R], "count": hdr[1 + R:1 + 2 * R],
-            "deg": hdr[1 + 2 * R:1 + 3 * R], "p0": hdr[1 + 3 * R:1 + 4 * R], "stride": hdr[1 + 4 * R:1 + 5 * R],
-            "ftab": raw[ot.value:ot.value + 4 * 8 * 64 * 8].view(np.uint32).reshape(8 * 64, 8),
-            "chk": raw[oc:oc + 2 * 8 * 64].view(np.int16),
-            "label": raw[ol.value:ol.value + 2 * code.n].view(np.uint16), "qc": bool(qc.value)}
 
 
 def timing_enable(on=True):

@@ -269,7 +269,6 @@ struct LaunchCfg {
   bool lblob = false;  // uses the layer-ordered blob (ms_layered_kernel)
   bool gtab = false;     // ms_flood_kernel: global tables, LDS = wave state only
   bool tlg = false;      // bp_team_lg_kernel: every table global, LDS image = layer pointers
-  bool cc = false;       // ms_layered_cc_kernel: compressed check records
   int team = 0;          // bp_team_kernel: waves per half-shot (one workgroup), 0 = wave kernels
   const char* name = "";  // kernel name as rocprofv3 reports it
   bool ok = false;
@@ -286,7 +285,7 @@ struct qldpc_schedule {
   std::vector<uint8_t> lblob;
   unsigned char* d_lblob = nullptr;
   int l_off_ltab = 0, l_off_lrow = 0, l_off_lay_ptr = 0, l_off_adj_ptr = 0, l_off_adj_vars = 0,
-      l_off_adj_info = 0, l_off_adj_dmax = 0, l_off_vn_chk = 0, l_off_vn_ck = 0;
+      l_off_adj_info = 0, l_off_adj_dmax = 0, l_off_vn_chk = 0;
   int off_cn_tab = 0, off_row_ptr = 0, off_vn_ptr = 0, off_vn_chk = 0;
   int off_lay_ptr = 0, off_lay_rows = 0, off_adj_ptr = 0, off_adj_vars = 0, off_chunk_dmax = 0;
   unsigned char* d_blob = nullptr;
@@ -298,9 +297,7 @@ struct qldpc_schedule {
   // flooding MS, uniform degree: global table image of ms_flood_kernel
   std::vector<uint8_t> fblob;
   unsigned char* d_fblob = nullptr;
-  int f_off_tab = 0, f_off_label = 0;
-  int f_n_post = 0, f_n_c2v = 0;  // LDS doubles (post labels) / floats (message slots) per wave
-  bool f_qc = false;              // bank-conflict-free lift-16 layout (flood_qc16_layout)
+  int f_off_tab = 0;
   LaunchCfg cfg[2];           // per algo
   std::mutex mu;
   // HBM-resident kernel (hbm_kernels.hip): 32-bit layer tables and a grow-only
@@ -334,241 +331,6 @@ static int put(std::vector<uint8_t>& blob, const std::vector<T>& v) {
   blob.resize(off + sizeof(T) * v.size());
   if (!v.empty()) memcpy(blob.data() + off, v.data(), sizeof(T) * v.size());
   return off;
-}
-
-// ---------------------------------------------------------------------------
-// ms_flood_kernel's global image (decoder_kernels.hip, FloodRuns): runs header
-// | edge words ftab[(lane + 64 slot) * 8 + k] = (4 * message slot) << 16 |
-// (8 * post label) | chk[lane + 64 slot] (check index, -1 = pad lane) |
-// label[original column]. Both layouts give identical results: only where in
-// the wave's LDS slice a value lives, and which lane updates which check,
-// change (the check-node update is order-independent: exact min / min2 and
-// XOR sign products).
-// ---------------------------------------------------------------------------
-struct FloodLayout {
-  std::vector<int32_t> hdr;   // n_runs, start[R], count[R], deg[R], p0[R], stride[R], off_chk
-  std::vector<uint32_t> ftab;
-  std::vector<int16_t> chk;
-  std::vector<uint16_t> label;
-  int n_post = 0, n_c2v = 0;
-};
-
-// The CSC layout: post label = the code's degree relabeling, message t of a
-// variable at its CSC position, check c on lane c % 64 of slot c / 64; pads
-// read post[0] and write the 8 floats behind the messages.
-static bool flood_plain_layout(const qldpc_code* code, FloodLayout* F) {
-  const int m = code->m, n = code->n;
-  F->hdr.assign(2 + 5 * QLDPC_MAX_RUNS, 0);
-  int nr = 0;
-  for (int j = 0; j < n;) {
-    const int d = code->csc_ptr[j + 1] - code->csc_ptr[j];
-    int e = j;
-    while (e < n && code->csc_ptr[e + 1] - code->csc_ptr[e] == d) ++e;
-    if (nr == QLDPC_MAX_RUNS) return false;
-    F->hdr[1 + nr] = j;
-    F->hdr[1 + QLDPC_MAX_RUNS + nr] = e - j;
-    F->hdr[1 + 2 * QLDPC_MAX_RUNS + nr] = d;
-    F->hdr[1 + 3 * QLDPC_MAX_RUNS + nr] = code->csc_ptr[j];
-    ++nr;
-    j = e;
-  }
-  F->hdr[0] = nr;
-  F->ftab.assign((size_t)8 * 64 * 8, 0);
-  F->chk.assign(8 * 64, -1);
-  for (int r = 0; r < 8 * 64; ++r) {
-    if (r < m) F->chk[r] = (int16_t)r;
-    for (int k = 0; k < 8; ++k) {
-      const int e = r < m ? code->row_ptr[r] + k : -1;
-      if (r < m && e < code->row_ptr[r + 1])
-        F->ftab[(size_t)8 * r + k] = ((uint32_t)(4 * code->edge_pos[e]) << 16) |
-                                     (uint32_t)(8 * code->vinv[code->col_idx[e]]);
-      else if (r >= m)
-        F->ftab[(size_t)8 * r + k] = (uint32_t)(4 * (code->E + k)) << 16;
-    }
-  }
-  F->label.assign(code->vinv.begin(), code->vinv.end());
-  F->n_post = n;
-  F->n_c2v = code->E + 8;
-  return true;
-}
-
-// Bank-conflict-free layout for quasi-cyclic codes of lift 16 (every 16 x 16
-// block of H zero or a permutation matrix: LP118_0, the headline code).
-// LDS serves a 32-lane group per cycle from 32 banks (post f64: label mod 32,
-// message f32: slot mod 32). Then:
-//  * labels: runs of equal column degree, each starting at a multiple of 32,
-//    block column C at label start + 16 b(C) + j; message t of label
-//    start + o at p0 + t S + o with S and p0 multiples of 32. A block's 16
-//    labels and its 16 messages of any one check row are then one half (16
-//    banks) of the 32, the same half: lambda(C) = b(C) mod 2.
-//  * two block rows share a 32-lane group (one lane per row); at edge round k
-//    they visit block columns of opposite lambda, so the group's 32 post
-//    reads, message reads and writes each hit 32 distinct banks.
-// A pairing exists when the rows' counts of lambda = 0 blocks sum to the row
-// degree; lambda is searched by random block orders inside the runs (a few
-// tries for LP118_0's Hx and Hz). Odd row counts leave one block row with
-// pad lanes placed in the other half.
-static bool flood_qc16_layout(const qldpc_code* code, FloodLayout* F) {
-  const int Z = 16, m = code->m, n = code->n, DC = code->uniform_deg;
-  if (m % Z || n % Z || DC < 1 || DC > 8) return false;
-  const int BR = m / Z, BC = n / Z;
-  std::vector<int> cnt((size_t)BR * BC, 0);
-  for (int r = 0; r < m; ++r) {
-    std::vector<int> seen;
-    for (int e = code->row_ptr[r]; e < code->row_ptr[r + 1]; ++e) {
-      const int C = code->col_idx[e] / Z;
-      if (std::find(seen.begin(), seen.end(), C) != seen.end()) return false;   // two ones in a block row
-      seen.push_back(C);
-      ++cnt[(size_t)(r / Z) * BC + C];
-    }
-  }
-  std::vector<int> col_blk(n, 0);            // per column: bitmask check of one one per block row
-  std::vector<std::vector<int>> colchk(n);   // checks of each column, ascending
-  for (int r = 0; r < m; ++r)
-    for (int e = code->row_ptr[r]; e < code->row_ptr[r + 1]; ++e) colchk[code->col_idx[e]].push_back(r);
-  for (int j = 0; j < n; ++j)
-    for (size_t q = 1; q < colchk[j].size(); ++q)
-      if (colchk[j][q] / Z == colchk[j][q - 1] / Z) return false;              // two ones in a block column
-  std::vector<std::vector<int>> rowblk(BR);
-  std::vector<int> bdeg(BC, 0);
-  for (int R = 0; R < BR; ++R)
-    for (int C = 0; C < BC; ++C) {
-      const int c = cnt[(size_t)R * BC + C];
-      if (c == 0) continue;
-      if (c != Z) return false;
-      rowblk[R].push_back(C);
-      ++bdeg[C];
-    }
-  for (int R = 0; R < BR; ++R)
-    if ((int)rowblk[R].size() != DC) return false;
-  // runs by ascending block-column degree
-  std::vector<int> degs(bdeg.begin(), bdeg.end());
-  std::sort(degs.begin(), degs.end());
-  degs.erase(std::unique(degs.begin(), degs.end()), degs.end());
-  if ((int)degs.size() > QLDPC_MAX_RUNS) return false;
-  std::vector<std::vector<int>> runs(degs.size());
-  for (int C = 0; C < BC; ++C)
-    runs[std::lower_bound(degs.begin(), degs.end(), bdeg[C]) - degs.begin()].push_back(C);
-  if ((int)runs[0].size() * Z < 32) return false;                                  // pads read labels 0..31
-  // search lambda (block order inside each run) admitting a row pairing
-  uint64_t rng = 0x9e3779b97f4a7c15ull;
-  auto rnd = [&](uint64_t k) {
-    rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
-    return (int)(rng % k);
-  };
-  std::vector<int> pos(BC), lam(BC);
-  std::vector<std::pair<int, int>> groups;   // (R1, R2), R2 = -1: single block row
-  for (int attempt = 0; attempt < 20000 && groups.empty(); ++attempt) {
-    for (auto& rc : runs) {
-      for (int q = (int)rc.size() - 1; q > 0; --q) std::swap(rc[q], rc[rnd(q + 1)]);
-      for (int b = 0; b < (int)rc.size(); ++b) {
-        pos[rc[b]] = b;
-        lam[rc[b]] = b & 1;
-      }
-    }
-    std::vector<std::vector<int>> by(DC + 1);
-    for (int R = 0; R < BR; ++R) {
-      int c0 = 0;
-      for (int C : rowblk[R]) c0 += lam[C] == 0;
-      by[c0].push_back(R);
-    }
-    for (int single = (BR & 1) ? 0 : -1; single <= ((BR & 1) ? DC : -1) && groups.empty(); ++single) {
-      if (single >= 0 && by[single].empty()) continue;
-      std::vector<std::vector<int>> b2 = by;
-      int sr = -1;
-      if (single >= 0) {
-        sr = b2[single].back();
-        b2[single].pop_back();
-      }
-      bool ok = true;
-      for (int x = 0; 2 * x <= DC && ok; ++x)
-        ok = (2 * x == DC) ? b2[x].size() % 2 == 0 : b2[x].size() == b2[DC - x].size();
-      if (!ok) continue;
-      for (int x = 0; 2 * x <= DC; ++x) {
-        if (2 * x == DC)
-          for (size_t q = 0; q + 1 < b2[x].size(); q += 2) groups.push_back({b2[x][q], b2[x][q + 1]});
-        else
-          for (size_t q = 0; q < b2[x].size(); ++q) groups.push_back({b2[x][q], b2[DC - x][q]});
-      }
-      if (sr >= 0) groups.push_back({sr, -1});
-    }
-  }
-  const int KC = (m + 63) / 64;
-  if (groups.empty() || (int)groups.size() > 2 * KC) return false;
-  // labels and message slots
-  F->hdr.assign(2 + 5 * QLDPC_MAX_RUNS, 0);
-  F->hdr[0] = (int)runs.size();
-  std::vector<int> run_of(BC), lab_start(runs.size()), msg_p0(runs.size()), msg_S(runs.size());
-  int next_label = 0, next_msg = 0;
-  for (size_t q = 0; q < runs.size(); ++q) {
-    const int count = Z * (int)runs[q].size(), K = degs[q];
-    const int S = K > 0 ? (count + 31) / 32 * 32 : 0;
-    lab_start[q] = next_label;
-    msg_p0[q] = next_msg;
-    msg_S[q] = S;
-    for (int C : runs[q]) run_of[C] = (int)q;
-    F->hdr[1 + q] = next_label;
-    F->hdr[1 + QLDPC_MAX_RUNS + q] = count;
-    F->hdr[1 + 2 * QLDPC_MAX_RUNS + q] = K;
-    F->hdr[1 + 3 * QLDPC_MAX_RUNS + q] = next_msg;
-    F->hdr[1 + 4 * QLDPC_MAX_RUNS + q] = S;
-    next_label = (next_label + count + 31) / 32 * 32;
-    next_msg += K * S;
-  }
-  const int scratch = next_msg;                // 32 pad-lane slots, two 16-bank halves
-  F->n_post = next_label;
-  F->n_c2v = next_msg + 32;
-  if (8 * F->n_post > 65535 || 4 * F->n_c2v > 65535) return false;
-  F->label.assign(n, 0);
-  for (int j = 0; j < n; ++j) {
-    const int C = j / Z, q = run_of[C];
-    F->label[j] = (uint16_t)(lab_start[q] + Z * pos[C] + j % Z);
-  }
-  auto word = [&](int r, int C) -> uint32_t {   // edge of check r in block column C
-    for (int e = code->row_ptr[r]; e < code->row_ptr[r + 1]; ++e) {
-      const int j = code->col_idx[e];
-      if (j / Z != C) continue;
-      const int q = run_of[C];
-      const int t = (int)(std::find(colchk[j].begin(), colchk[j].end(), r) - colchk[j].begin());
-      const int slot = msg_p0[q] + t * msg_S[q] + Z * pos[C] + j % Z;
-      return ((uint32_t)(4 * slot) << 16) | (uint32_t)(8 * F->label[j]);
-    }
-    return 0;
-  };
-  F->ftab.assign((size_t)8 * 64 * 8, 0);
-  F->chk.assign(8 * 64, -1);
-  for (int g = 0; g < 2 * KC; ++g) {
-    const int base = 64 * (g >> 1) + 32 * (g & 1);   // lane + 64 slot of the group's first lane
-    std::vector<std::pair<int, int>> match;          // per round: (block of R1, block of R2)
-    const int R1 = g < (int)groups.size() ? groups[g].first : -1;
-    const int R2 = g < (int)groups.size() ? groups[g].second : -1;
-    if (R1 >= 0 && R2 >= 0) {
-      std::vector<int> z1, o1, z2, o2;
-      for (int C : rowblk[R1]) (lam[C] ? o1 : z1).push_back(C);
-      for (int C : rowblk[R2]) (lam[C] ? o2 : z2).push_back(C);
-      for (size_t q = 0; q < z1.size(); ++q) match.push_back({z1[q], o2[q]});
-      for (size_t q = 0; q < o1.size(); ++q) match.push_back({o1[q], z2[q]});
-    } else if (R1 >= 0) {
-      for (int C : rowblk[R1]) match.push_back({C, -1});
-    }
-    for (int l = 0; l < 32; ++l) {
-      const int R = l < Z ? R1 : R2, jr = l % Z;
-      uint32_t* w = &F->ftab[(size_t)8 * (base + l)];
-      if (R >= 0) {
-        const int r = R * Z + jr;
-        F->chk[base + l] = (int16_t)r;
-        for (int k = 0; k < DC; ++k) w[k] = word(r, l < Z ? match[k].first : match[k].second);
-      } else {
-        // pad lane: the half of the banks its live partner group leaves free
-        for (int k = 0; k < 8; ++k) {
-          const int h = (R1 >= 0 && k < DC) ? 1 - lam[match[k].first] : (l >> 4);
-          const int o = 16 * h + jr;
-          w[k] = ((uint32_t)(4 * (scratch + o)) << 16) | (uint32_t)(8 * o);
-        }
-      }
-    }
-  }
-  return true;
 }
 
 extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const int32_t* h_layer_ptr,
@@ -751,32 +513,44 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
       s->l_off_adj_info = put(s->lblob, adj_info);
       s->l_off_adj_dmax = put(s->lblob, adj_dmax);
       s->l_off_vn_chk = put(s->lblob, code->avar);   // filter word per relabeled variable
-      if (16 * m < 65536) {
-        // ms_layered_cc_kernel: per CSC position 16 * check + edge index (its
-        // record and message), 8 pad entries for the unrolled VN reads
-        std::vector<uint16_t> vn_ck(code->E + 8, 0);
-        for (int r = 0; r < m; ++r)
-          for (int e = code->row_ptr[r]; e < code->row_ptr[r + 1]; ++e)
-            vn_ck[code->edge_pos[e]] = (uint16_t)(16 * r + (e - code->row_ptr[r]));
-        s->l_off_vn_ck = put(s->lblob, vn_ck);
-      }
       s->lblob.resize(align16((int)s->lblob.size() + 1));
     }
   }
   if (!s->layered && fast_table_ok(code) && m <= 8 * 64) {
-    FloodLayout F;
-    const bool qc = !getenv("QLDPC_FLOOD_PLAIN") && flood_qc16_layout(code, &F);
-    if (qc || flood_plain_layout(code, &F)) {
-      F.hdr[1 + 5 * QLDPC_MAX_RUNS] = 0;
-      (void)put(s->fblob, F.hdr);
-      s->f_off_tab = put(s->fblob, F.ftab);
-      const int off_chk = put(s->fblob, F.chk);
-      memcpy(s->fblob.data() + sizeof(int32_t) * (1 + 5 * QLDPC_MAX_RUNS), &off_chk, sizeof(int32_t));
-      s->f_off_label = put(s->fblob, F.label);
+    // ms_flood_kernel's global image: FloodRuns header (runs of equal column
+    // degree over the relabeled variables), then per check c = lane + 64 i the
+    // words [8c, 8c+8): (4 * csc position) << 16 | (8 * relabeled variable).
+    // Pad checks write the pad floats E..E+7 behind c2v and read post[0].
+    std::vector<int32_t> hdr(1 + 4 * QLDPC_MAX_RUNS, 0);
+    int nr = 0;
+    bool ok = true;
+    for (int j = 0; j < n;) {
+      const int d = code->csc_ptr[j + 1] - code->csc_ptr[j];
+      int e = j;
+      while (e < n && code->csc_ptr[e + 1] - code->csc_ptr[e] == d) ++e;
+      if (nr == QLDPC_MAX_RUNS) { ok = false; break; }
+      hdr[1 + nr] = j;                                   // start
+      hdr[1 + QLDPC_MAX_RUNS + nr] = e - j;              // count
+      hdr[1 + 2 * QLDPC_MAX_RUNS + nr] = d;              // degree
+      hdr[1 + 3 * QLDPC_MAX_RUNS + nr] = code->csc_ptr[j];  // csc start
+      ++nr;
+      j = e;
+    }
+    hdr[0] = nr;
+    if (ok) {
+      std::vector<uint32_t> ftab((size_t)8 * 64 * 8, 0);
+      for (int r = 0; r < 8 * 64; ++r)
+        for (int k = 0; k < 8; ++k) {
+          const int e = r < m ? code->row_ptr[r] + k : -1;
+          if (r < m && e < code->row_ptr[r + 1])
+            ftab[(size_t)8 * r + k] = ((uint32_t)(4 * code->edge_pos[e]) << 16) |
+                                      (uint32_t)(8 * code->vinv[code->col_idx[e]]);
+          else if (r >= m)
+            ftab[(size_t)8 * r + k] = (uint32_t)(4 * (code->E + k)) << 16;
+        }
+      (void)put(s->fblob, hdr);
+      s->f_off_tab = put(s->fblob, ftab);
       s->fblob.resize(align16((int)s->fblob.size() + 1));
-      s->f_n_post = F.n_post;
-      s->f_n_c2v = F.n_c2v;
-      s->f_qc = qc;
     }
   }
   }  // s->lds_ok
@@ -833,17 +607,6 @@ extern "C" int qldpc_schedule_destroy(qldpc_schedule* s) {
   return QLDPC_OK;
 }
 
-extern "C" int qldpc_schedule_flood_image(const qldpc_schedule* s, const uint8_t** image, int* bytes, int* off_tab,
-                                          int* off_label, int* qc_layout) {
-  if (!s || !image || !bytes || !off_tab || !off_label || !qc_layout) return fail(QLDPC_EINVAL, "null argument");
-  *image = s->fblob.empty() ? nullptr : s->fblob.data();
-  *bytes = (int)s->fblob.size();
-  *off_tab = s->f_off_tab;
-  *off_label = s->f_off_label;
-  *qc_layout = s->f_qc ? 1 : 0;
-  return QLDPC_OK;
-}
-
 // per-wave state slice: post f64[n] | c2v (f32|f64)[E] | syn words | parity words
 static void wave_layout(const qldpc_code* c, bool layered, int algo, int* bytes, int* off_c2v,
                         int* off_synw, int* off_parw, bool colsum_f32 = false) {
@@ -875,19 +638,6 @@ static void team_layout(const qldpc_code* c, int w, int* bytes, int* off_c2v, in
   *bytes = off;
 }
 
-// ms_flood_kernel's slice: post f64[f_n_post] | messages f32[f_n_c2v]
-static void flood_wave_layout(const qldpc_schedule* s, int* bytes, int* off_c2v) {
-  *off_c2v = align16(8 * s->f_n_post);
-  *bytes = align16(*off_c2v + 4 * s->f_n_c2v);
-}
-
-// ms_layered_cc_kernel's slice: column sums f32[n] | records uint4[m] | syn words
-static void cc_wave_layout(const qldpc_code* c, int* bytes, int* off_rec, int* off_synw) {
-  *off_rec = align16(4 * c->n);
-  *off_synw = align16(*off_rec + 16 * c->m);
-  *bytes = align16(*off_synw + 4 * 2 * ((c->m + 63) / 64));
-}
-
 static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   std::lock_guard<std::mutex> lk(s->mu);
   LaunchCfg& cfg = s->cfg[algo];
@@ -916,12 +666,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
     if (const char* ev = getenv("QLDPC_MS_LANES_PER_CHECK")) g = atoi(ev);
     // (several half-shots per wave, ms_layered_grp_kernel, measured 2x slower
     // in round 2: at a fixed LDS budget it halves the waves per CU; removed)
-    if (g == 1 && s->l_off_vn_ck > 0 && !getenv("QLDPC_MS_C2V_FULL")) {
-      cfg.kernel = qldpc::select_ms_layered_cc_kernel(dc, &cfg.name);
-      cfg.cc = cfg.kernel != nullptr;
-      if (cfg.cc) max_waves = 16;
-    }
-    if (!cfg.kernel) cfg.kernel = qldpc::select_ms_layered_kernel(dc, g, &cfg.name);
+    cfg.kernel = qldpc::select_ms_layered_kernel(dc, g, &cfg.name);
     use_lblob = cfg.kernel != nullptr;
   }
   cfg.lblob = use_lblob;
@@ -956,8 +701,6 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   int off_c2v, off_synw, off_parw, off_red;
   wave_layout(c, s->layered, algo, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw, use_lblob);
   if (team) team_layout(c, team, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw, &off_red);
-  if (gtab) flood_wave_layout(s, &cfg.wave_bytes, &off_c2v);
-  if (cfg.cc) cc_wave_layout(c, &cfg.wave_bytes, &off_c2v, &off_synw);
   int max_lds = 0, dev = 0;
   HIP_TRY(hipGetDevice(&dev));
   HIP_TRY(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
@@ -1242,10 +985,6 @@ extern "C" int qldpc_decode_device_ex(const qldpc_code* code, const qldpc_schedu
     a.off_row_ptr = sched->l_off_adj_info;
     a.off_chunk_dmax = sched->l_off_adj_dmax;
     a.off_vn_chk = sched->l_off_vn_chk;
-    if (cfg->cc) {
-      a.off_vn_ptr = sched->l_off_vn_ck;
-      cc_wave_layout(code, &a.wave_bytes, &a.off_c2v, &a.off_synw);
-    }
   }
   if (cfg->team) team_layout(code, cfg->team, &a.wave_bytes, &a.off_c2v, &a.off_synw, &a.off_parw, &a.off_red);
   if (cfg->tlg) {  // bp_team_lg_kernel: layer pointers in LDS, every table global
@@ -1261,13 +1000,12 @@ extern "C" int qldpc_decode_device_ex(const qldpc_code* code, const qldpc_schedu
     a.blob = sched->d_fblob;
     a.blob_bytes = 0;
     a.off_cn_tab = sched->f_off_tab;
-    flood_wave_layout(sched, &a.wave_bytes, &a.off_c2v);
   }
   a.m = code->m;
   a.n = code->n;
   a.E = code->E;
   a.n_layers = sched->n_layers;
-  a.vinv = cfg->gtab ? (const uint16_t*)(sched->d_fblob + sched->f_off_label) : code->d_vinv;
+  a.vinv = code->d_vinv;
   a.syn = (const uint8_t*)d_syn;
   a.ehat = (uint8_t*)d_ehat;
   a.syn_bits = syn_format == QLDPC_FMT_BITS;

@@ -7,7 +7,7 @@
 #define QLDPC_MAX_THREADS 768
 // max runs of equal column degree the flooding MS kernel handles
 #define QLDPC_MAX_RUNS 8
-#define QLDPC_FLOOD_HDR 160  // LDS bytes of ms_flood_kernel's runs header (5 * 8 ints)
+#define QLDPC_FLOOD_HDR 128  // LDS bytes of ms_flood_kernel's runs header (4 * 8 ints)
 
 namespace qldpc {
 
@@ -58,8 +58,6 @@ const void* select_ms_flood_kernel(int dc, int kc, const char** name);  // nullp
 int ms_flood_max_waves(int kc);                      // waves per workgroup it was compiled for
 // layered MS, uniform row degree 7/8, G = 1/2/4/8 lanes per check (layer-table blob)
 const void* select_ms_layered_kernel(int dc, int g, const char** name);
-// layered MS, one lane per check, compressed check records (vn_ck in the layer blob)
-const void* select_ms_layered_cc_kernel(int dc, const char** name);
 // layered BP teams, every graph table in global memory (gblob of the schedule)
 const void* select_bp_team_lg_kernel(int dc, int w, const char** name);
 // BP, uniform row degree 7/8: one team of W waves per half-shot, edge-parallel check nodes

@@ -860,15 +860,9 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) decode_kernel(DecodeArgs a)
 //    addressing. Pad checks (c >= m) read post[0] and write the 8-float pad
 //    behind c2v; `livem` masks their flags.
 //  * Variable nodes are visited by runs of equal column degree K (variables
-//    are relabeled by degree): no per-variable table, no masking, a
-//    compile-time K. Message t of variable start + o sits at p0 + o * K + t
-//    (stride 0: the CSC order) or, in the bank-conflict-free layout of
-//    quasi-cyclic lift-16 codes (capi.cpp flood_qc16_layout),
-//    at p0 + t * stride + o.
-//  * Lane / slot i of the wave owns check chk[lane + 64 i] (-1 = pad): the
-//    QC layout pairs block rows so that every LDS access of the check node is
-//    conflict-free, which fixes which lanes hold which checks.
-// The LDS then holds only wave state: post f64[labels] | c2v f32[slots].
+//    are relabeled by degree, so the CSC start of variable start + o is
+//    p0 + o * K): no per-variable table, no masking, a compile-time K.
+// The LDS then holds only wave state: post f64[n] | c2v f32[E + 8].
 // ---------------------------------------------------------------------------
 // Per-lane edge addresses of the KC checks a lane owns: absolute LDS byte
 // addresses, 16 VGPRs per check, no VALU per use.
@@ -901,8 +895,6 @@ struct FloodTab {
 struct FloodRuns {  // fblob header: runs of equal column degree (capi.cpp)
   int n_runs;
   int start[QLDPC_MAX_RUNS], count[QLDPC_MAX_RUNS], deg[QLDPC_MAX_RUNS], p0[QLDPC_MAX_RUNS];
-  int stride[QLDPC_MAX_RUNS];  // 0: message t of variable o at p0 + o K + t; else p0 + t stride + o
-  int off_chk;                 // fblob byte offset of int16 chk[8 * 64]: check of (lane, slot), -1 = pad
 };
 
 // Sequential float32 sum in ascending check order (np.sum axis=0). It starts
@@ -945,29 +937,6 @@ __device__ __forceinline__ void vn_run(const DecodeArgs& a, double* post, const 
   if (o0 + lane < count) po[o0] = a.L + (double)vn_sum<K>(c + o0 * K);
 }
 
-// slot-major run: message t of variable start + o at p0 + t * S + o (S a
-// multiple of 32): each read of a 64-variable chunk is 64 consecutive floats
-template <int K>
-__device__ __forceinline__ void vn_run_sm(const DecodeArgs& a, double* post, const float* c2v,
-                                          int start, int count, int p0, int S, int lane) {
-  const float* c = c2v + p0 + lane;
-  double* po = post + start + lane;
-  auto sum = [&](int o0) {
-    float s = c[o0];
-#pragma unroll
-    for (int t = 1; t < K; ++t) s += c[o0 + t * S];     // float32, ascending check
-    return s;
-  };
-  int o0 = 0;
-  for (; o0 + 128 <= count; o0 += 128) {
-    const float s0 = sum(o0), s1 = sum(o0 + 64);
-    po[o0] = a.L + (double)s0;
-    po[o0 + 64] = a.L + (double)s1;
-  }
-  for (; o0 + 64 <= count; o0 += 64) po[o0] = a.L + (double)sum(o0);
-  if (o0 + lane < count) po[o0] = a.L + (double)sum(o0);
-}
-
 __device__ __forceinline__ void vn_run_any(const DecodeArgs& a, double* post, const float* c2v,
                                            int start, int count, int K, int p0, int lane) {
   for (int o = lane; o < count; o += 64) {
@@ -1000,23 +969,19 @@ ms_flood_kernel(DecodeArgs a) {
   double* post = (double*)ws;
   unsigned char* c2v_b = ws + a.off_c2v;
   const float* c2v_f = (const float*)c2v_b;
-  const int n = a.n;
+  const int m = a.m, n = a.n;
 
   // static per-lane graph data (VGPRs for the kernel)
   FloodTab<KC> tab;
   tab.init(ftab, lane, lds_addr(ws), lds_addr(ws) + (uint32_t)a.off_c2v);
-  const int16_t* chk = (const int16_t*)(a.blob + __builtin_amdgcn_readfirstlane(runs->off_chk));
-  int lchk[KC];
   uint32_t livem = 0;
 #pragma unroll
-  for (int i = 0; i < KC; ++i) {
-    lchk[i] = chk[lane + 64 * i];
-    if (lchk[i] >= 0) livem |= 1u << i;
-  }
+  for (int i = 0; i < KC; ++i)
+    if (lane + 64 * i < m) livem |= 1u << i;
   // the runs header lives in LDS (the first QLDPC_FLOOD_HDR bytes): one
   // broadcast read per field per iteration, no global latency in the loop
   const int n_runs = __builtin_amdgcn_readfirstlane(runs->n_runs);
-  if (threadIdx.x < 5 * QLDPC_MAX_RUNS) ((int*)lds)[threadIdx.x] = (&runs->start[0])[threadIdx.x];
+  if (threadIdx.x < 4 * QLDPC_MAX_RUNS) ((int*)lds)[threadIdx.x] = (&runs->start[0])[threadIdx.x];
   __syncthreads();
   const int* hdr = (const int*)lds;
 
@@ -1028,8 +993,10 @@ ms_flood_kernel(DecodeArgs a) {
     bool conv = false;
     uint32_t synreg = 0;
 #pragma unroll
-    for (int i = 0; i < KC; ++i)
-      if (lchk[i] >= 0) synreg |= syn_bit(a, hs, lchk[i]) << i;
+    for (int i = 0; i < KC; ++i) {
+      const int c = lane + 64 * i;
+      if (c < m) synreg |= syn_bit(a, hs, c) << i;
+    }
     for (int it = 0;; ++it) {
       uint32_t unsat = 0;
       if (it == 0) {
@@ -1069,25 +1036,6 @@ ms_flood_kernel(DecodeArgs a) {
         const int cnt = __builtin_amdgcn_readfirstlane(hdr[QLDPC_MAX_RUNS + r]);
         const int K = __builtin_amdgcn_readfirstlane(hdr[2 * QLDPC_MAX_RUNS + r]);
         const int p0 = __builtin_amdgcn_readfirstlane(hdr[3 * QLDPC_MAX_RUNS + r]);
-        const int S = __builtin_amdgcn_readfirstlane(hdr[4 * QLDPC_MAX_RUNS + r]);
-        if (S) {
-          switch (K) {
-            case 0: vn_run<0>(a, post, c2v_f, st, cnt, p0, lane); break;
-            case 1: vn_run<1>(a, post, c2v_f, st, cnt, p0, lane); break;
-            case 2: vn_run_sm<2>(a, post, c2v_f, st, cnt, p0, S, lane); break;
-            case 3: vn_run_sm<3>(a, post, c2v_f, st, cnt, p0, S, lane); break;
-            case 4: vn_run_sm<4>(a, post, c2v_f, st, cnt, p0, S, lane); break;
-            case 5: vn_run_sm<5>(a, post, c2v_f, st, cnt, p0, S, lane); break;
-            case 6: vn_run_sm<6>(a, post, c2v_f, st, cnt, p0, S, lane); break;
-            default:
-              for (int o = lane; o < cnt; o += 64) {
-                float sv = 0.0f;
-                for (int t = 0; t < K; ++t) sv += c2v_f[p0 + t * S + o];
-                post[st + o] = a.L + (double)sv;
-              }
-          }
-          continue;
-        }
         switch (K) {
           case 0: vn_run<0>(a, post, c2v_f, st, cnt, p0, lane); break;
           case 1: vn_run<1>(a, post, c2v_f, st, cnt, p0, lane); break;
@@ -1464,229 +1412,6 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
       }
     }
     {                                                          // ê, posteriors in original order
-      double* po = a.post ? a.post + hs * (long long)n : nullptr;
-      for (int k = 0; k < 16 && 64 * k < n; ++k) {
-        const int jo = 64 * k + lane;
-        if (jo < n) {
-          const double pv = L + (double)colS[n <= 1024 ? vr.get(k) : a.vinv[jo]];
-          put_ehat(a, hs, jo, pv < 0.0);
-          if (po) po[jo] = pv;
-        }
-      }
-      for (int jo = 1024 + lane; jo < n; jo += 64) {
-        const double pv = L + (double)colS[a.vinv[jo]];
-        put_ehat(a, hs, jo, pv < 0.0);
-        if (po) po[jo] = pv;
-      }
-    }
-    const uint64_t b1 = ballot((fl & FLAG_MIN_ZERO) != 0);
-    if (lane == 0) {
-      a.iters[hs] = iters;
-      if (a.flags) a.flags[hs] = (int32_t)((b1 ? FLAG_MIN_ZERO : 0) | (conv ? FLAG_CONVERGED : 0));
-    }
-    wave_sync();
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Layered min-sum with compressed check records (one lane per check; the
-// configs[3] decoder, LP118_2's 30- and 60-row layers). Same arithmetic and
-// results as ms_layered_kernel, bit for bit. A check's outgoing min-sum
-// messages take two magnitudes with one common sign, so the per-wave state
-// keeps per check c one 16-byte record instead of DC floats:
-//   rec[c] = {c1n, c2n, bits}: message of edge k = (bit k ? c2n : c1n) with
-//   its sign flipped by bit 8 + k        (cn_ms_compute's c2v_e, :167-168)
-// LP118_2: 7.2 KB of records instead of 14.4 KB of messages, so a CU holds
-// ~1.7x the half-shots (the kernel is latency-bound: 6 waves per CU left
-// VALU 45 % busy). The check node reads one record instead of DC messages;
-// the variable node decodes each term from its check's record, located by
-// the per-CSC-position word 16 c + k (vn_ck, blob field off_vn_ptr).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ float cc_msg(const uint4& r, uint32_t k) {
-  const uint32_t mag = ((r.z >> k) & 1u) ? r.y : r.x;
-  return __builtin_bit_cast(float, mag ^ (((r.z >> (8u + k)) & 1u) << 31));
-}
-
-// check node of check c (ltab row t: low 16 bits = 4 * variable), one lane
-template <int DC>
-__device__ __forceinline__ void cn_ms_record(const DecodeArgs& a, const uint32_t (&t)[8], uint32_t synb, bool first,
-                                             uint32_t post_b, uint4* rec, int c, int& fl) {
-  if (first) {
-    // every v_e = float32(L) (:148-149): min1 = min2 = |L32|, sign_e = L32 < 0
-    const double vf = (double)a.L32;
-    const double av = __builtin_fabs(vf);
-    const uint32_t cb = __builtin_bit_cast(uint32_t, (float)(a.beta * av));
-    const uint32_t neg = (uint32_t)(vf < 0.0);
-    if (av == 0.0) fl |= FLAG_MIN_ZERO;
-    const uint32_t c1n = cb | ((((neg * DC) ^ synb) & 1u) << 31);
-    rec[c] = make_uint4(c1n, c1n, neg ? (((1u << DC) - 1u) << 8) : 0u, 0u);
-    return;
-  }
-  const uint4 r = rec[c];
-  double v[DC];
-  uint32_t hv[DC];
-#pragma unroll
-  for (int k = 0; k < DC; ++k) {
-    const double pj = a.L + (double)*QLDPC_LDS(const float, post_b + (t[k] & 0xffffu));   // (:173)
-    v[k] = pj - (double)cc_msg(r, (uint32_t)k);                                           // (:177)
-    hv[k] = hi_word(v[k]);
-  }
-  double min1, min2;
-  min12_tree<DC>(v, min1, min2);
-  const uint32_t sh = xor_tree<DC>(hv);
-  double m1 = min1, m2 = min2;
-  if (__builtin_expect(ballot((min1 == 0.0) | (min2 == __builtin_inf())) != 0, 0)) {
-    m1 = __builtin_isinf(min1) ? 0.0 : min1;              // (:165)
-    m2 = __builtin_isinf(min2) ? 0.0 : min2;              // (:166)
-    if (m1 == 0.0) fl |= FLAG_MIN_ZERO;
-  }
-  const uint32_t npm = ((sh >> 31) ^ synb) << 31;
-  const uint32_t c1n = __builtin_bit_cast(uint32_t, (float)(a.beta * m1)) ^ npm;
-  const uint32_t c2n = __builtin_bit_cast(uint32_t, (float)(a.beta * m2)) ^ npm;
-  uint32_t bits = 0;
-#pragma unroll
-  for (int k = 0; k < DC; ++k)
-    bits |= ((__builtin_fabs(v[k]) == min1) ? (1u << k) : 0u) | ((hv[k] >> 31) << (8 + k));
-  rec[c] = make_uint4(c1n, c2n, bits, 0u);
-}
-
-// variable node of one layer from the records (vn_layer's order and tests)
-template <int K>
-__device__ __forceinline__ uint32_t vn_layer_cc(const uint32_t* adj_info, const uint32_t* avar, float* colS,
-                                                const uint16_t* vn_ck, const unsigned char* recb, int v0, int v1,
-                                                int lane, float thr) {
-  uint32_t acc = 0;
-  for (int qb = v0; qb < v1; qb += 128) {
-    uint32_t info[2];
-    bool in[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int q = qb + 64 * h + lane;
-      in[h] = q < v1;
-      info[h] = adj_info[in[h] ? q : v0];
-    }
-    float old[2];
-    uint32_t av[2], kk[2][K];
-    uint4 r[2][K];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      old[h] = colS[info[h] >> 21];
-      av[h] = avar[info[h] >> 21];
-      const uint16_t* ck = vn_ck + (info[h] & 0xffffu);    // padded: t >= d reads a valid record
-#pragma unroll
-      for (int t = 0; t < K; ++t) {
-        const uint32_t w = ck[t];
-        kk[h][t] = w & 15u;
-        r[h][t] = *(const uint4*)(recb + (w & ~15u));
-      }
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int d = (int)((info[h] >> 16) & 31u);
-      float s = 0.0f;                                       // sequential, ascending check (:172)
-#pragma unroll
-      for (int t = 0; t < K; ++t) s += (t < d) ? cc_msg(r[h][t], kk[h][t]) : 0.0f;
-      if (in[h]) colS[info[h] >> 21] = s;
-      const bool flip = in[h] && ((old[h] < thr) != (s < thr));
-      acc ^= flip ? av[h] : 0u;
-    }
-  }
-  return acc;
-}
-
-template <int DC>
-__global__ void __launch_bounds__(1024) ms_layered_cc_kernel(DecodeArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  {
-    const uint4* src = (const uint4*)a.blob;
-    uint4* dst = (uint4*)lds;
-    const int nvec = a.blob_bytes >> 4;
-    for (int i = threadIdx.x; i < nvec; i += blockDim.x) dst[i] = src[i];
-  }
-  __syncthreads();
-  const uint32_t* ltab = (const uint32_t*)(lds + a.off_cn_tab);      // [Q][8]
-  const uint16_t* lrow = (const uint16_t*)(lds + a.off_lay_rows);    // [Q]
-  const uint16_t* lay_ptr = (const uint16_t*)(lds + a.off_lay_ptr);  // [L+1]
-  const uint16_t* adj_ptr = (const uint16_t*)(lds + a.off_adj_ptr);  // [L+1]
-  const uint32_t* adj_info = (const uint32_t*)(lds + a.off_row_ptr); // [A] var<<21 | deg<<16 | csc start
-  const uint8_t* adj_dmax = (const uint8_t*)(lds + a.off_chunk_dmax);// [L] max degree per layer
-  const uint32_t* avar = (const uint32_t*)(lds + a.off_vn_chk);      // [n] filter word per variable
-  const uint16_t* vn_ck = (const uint16_t*)(lds + a.off_vn_ptr);     // [E + 8] 16 * check + edge
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  const int waves = blockDim.x >> 6;
-  unsigned char* ws = lds + a.blob_bytes + wid * a.wave_bytes;
-  float* colS = (float*)ws;
-  uint4* rec = (uint4*)(ws + a.off_c2v);
-  uint32_t* synw = (uint32_t*)(ws + a.off_synw);
-  const uint32_t post_b = lds_addr(colS);
-  const int m = a.m, n = a.n;
-  const float thr = a.hd_thresh;
-  VinvRegs<16> vr;
-  vr.load(a.vinv, n, lane);
-
-  for (HalfShotQueue Q(a, waves, wid); Q.hs < a.batch; Q.advance()) {
-    const long long hs = Q.hs;
-    Q.prefetch(threadIdx.x & 63);
-    int fl = 0;
-    int iters = a.max_iter;
-    bool conv = false;
-    const double L = a.L;
-    load_syndrome_bits<8>(a, hs, synw, lane);
-    for (int j = lane; j < n; j += 64) colS[j] = 0.0f;          // post = L, c2v = 0 (:148-150)
-    for (int c = lane; c < m; c += 64) rec[c] = make_uint4(0u, 0u, 0u, 0u);
-    wave_sync();
-    uint32_t bl = 0;
-    for (int c = lane; c < m; c += 64) bl ^= ((synw[c >> 5] >> (c & 31)) & 1u) ? a.wc[c] : 0u;
-    const uint32_t B = wave_xor(bl);
-    uint32_t F = (L < 0.0) ? a.filt_all : 0u;
-    bool first = true;
-    for (int it = 0; it < a.max_iter && !conv; ++it) {
-      for (int l = 0; l < a.n_layers; ++l) {
-        const int q0 = lay_ptr[l], q1 = lay_ptr[l + 1];
-        for (int q = q0 + lane; q < q1; q += 64) {
-          uint32_t t[8];
-          load_row8(ltab + q * 8, t);
-          const int c = lrow[q];
-          cn_ms_record<DC>(a, t, (synw[c >> 5] >> (c & 31)) & 1u, first, post_b, rec, c, fl);
-        }
-        first = false;
-        wave_sync();
-        const int v0 = adj_ptr[l], v1 = adj_ptr[l + 1];
-        const int dmax = __builtin_amdgcn_readfirstlane((int)adj_dmax[l]) & 31;
-        const unsigned char* recb = (const unsigned char*)rec;
-        uint32_t acc = 0;
-        switch (dmax) {
-          case 1: acc = vn_layer_cc<1>(adj_info, avar, colS, vn_ck, recb, v0, v1, lane, thr); break;
-          case 2: acc = vn_layer_cc<2>(adj_info, avar, colS, vn_ck, recb, v0, v1, lane, thr); break;
-          case 3: acc = vn_layer_cc<3>(adj_info, avar, colS, vn_ck, recb, v0, v1, lane, thr); break;
-          case 4: acc = vn_layer_cc<4>(adj_info, avar, colS, vn_ck, recb, v0, v1, lane, thr); break;
-          case 5: acc = vn_layer_cc<5>(adj_info, avar, colS, vn_ck, recb, v0, v1, lane, thr); break;
-          case 6: acc = vn_layer_cc<6>(adj_info, avar, colS, vn_ck, recb, v0, v1, lane, thr); break;
-          default:
-            for (int q = v0 + lane; q < v1; q += 64) {
-              const uint32_t info = adj_info[q];
-              const int j = (int)(info >> 21), d = (int)((info >> 16) & 31u);
-              const float old = colS[j];
-              float sv = 0.0f;
-              for (int tt = 0; tt < d; ++tt) {
-                const uint32_t w = vn_ck[(info & 0xffffu) + tt];
-                sv += cc_msg(*(const uint4*)(recb + (w & ~15u)), w & 15u);
-              }
-              colS[j] = sv;
-              if ((old < thr) != (sv < thr)) acc ^= avar[j];
-            }
-        }
-        F ^= wave_xor(acc);
-        wave_sync();
-        if (F == B && layered_full_check<DC>(a, colS, synw, lane, thr)) {
-          iters = it + 1;
-          conv = true;
-          break;
-        }
-      }
-    }
-    {
       double* po = a.post ? a.post + hs * (long long)n : nullptr;
       for (int k = 0; k < 16 && 64 * k < n; ++k) {
         const int jo = 64 * k + lane;
@@ -2207,12 +1932,6 @@ const void* select_bp_team_lg_kernel(int dc, int w, const char** name) {
   if (dc == 8 && w == 4) QLDPC_NAMED((&bp_team_lg_kernel<8, 4>), "bp_team_lg_kernel<8, 4>");
   if (dc == 7 && w == 8) QLDPC_NAMED((&bp_team_lg_kernel<7, 8>), "bp_team_lg_kernel<7, 8>");
   if (dc == 8 && w == 8) QLDPC_NAMED((&bp_team_lg_kernel<8, 8>), "bp_team_lg_kernel<8, 8>");
-  return nullptr;
-}
-
-const void* select_ms_layered_cc_kernel(int dc, const char** name) {
-  if (dc == 7) QLDPC_NAMED((&ms_layered_cc_kernel<7>), "ms_layered_cc_kernel<7>");
-  if (dc == 8) QLDPC_NAMED((&ms_layered_cc_kernel<8>), "ms_layered_cc_kernel<8>");
   return nullptr;
 }
 

@@ -54,7 +54,7 @@ def test_bench_layered_channel_line():
                "--code", "LP118_2", "--schedule", "L", "--p", "0.05")
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
-    assert d["roofline"]["kernel"] in ("ms_layered_cc_kernel<8>", "ms_layered_kernel<8, 1>")
+    assert d["roofline"]["kernel"].startswith("ms_layered_kernel<8")
     assert 1.0 < d["config"]["avg_iterations"] < 10.0
 
 

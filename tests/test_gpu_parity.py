@@ -242,7 +242,7 @@ def test_decode_batch_into_preallocated_buffers(dec):
 
 
 
-KERNELS = ["G1", "G1full", "G2", "G4", "G8", "generic", "default"]
+KERNELS = ["G1", "G2", "G4", "G8", "generic", "default"]
 
 
 @pytest.mark.parametrize("code", ["LP118_2", "LP118_0", "LP04_0"])
@@ -250,20 +250,16 @@ KERNELS = ["G1", "G1full", "G2", "G4", "G8", "generic", "default"]
 def test_ms_layered_kernels_match_oracle(dec, kernel, code, monkeypatch):
     """Every layered MS kernel shape against the oracle, bit for bit, with
     fixed-work and channel syndromes mixed in one batch: ms_layered_kernel at
-    every lanes-per-check width G (QLDPC_MS_LANES_PER_CHECK; G = 1 is
-    ms_layered_cc_kernel, the compressed check records, and "G1full" the
-    per-edge messages, QLDPC_MS_C2V_FULL), the default per-layer choice, and
-    the generic decode kernel (QLDPC_NO_LAYERED_FAST). Lane mappings and
-    message storage never change the arithmetic."""
+    every lanes-per-check width G (QLDPC_MS_LANES_PER_CHECK), the default
+    per-layer choice, and the generic decode kernel (QLDPC_NO_LAYERED_FAST).
+    Lane mappings never change the arithmetic."""
     from oracle import oracle
     from qldpcsim_amd import _lib, codes, schedule
     Hx, Hz = codes.load_code(code)
     if kernel == "generic":
         monkeypatch.setenv("QLDPC_NO_LAYERED_FAST", "1")
     elif kernel.startswith("G"):
-        monkeypatch.setenv("QLDPC_MS_LANES_PER_CHECK", kernel[1:2])
-        if kernel == "G1full":
-            monkeypatch.setenv("QLDPC_MS_C2V_FULL", "1")
+        monkeypatch.setenv("QLDPC_MS_LANES_PER_CHECK", kernel[1:])
     lx, _ = schedule.select_layers(Hx, Hz, "L")
     lp, lr = schedule.pack_layers(lx, Hz.shape[0])
     rng = np.random.default_rng(11)
@@ -276,9 +272,7 @@ def test_ms_layered_kernels_match_oracle(dec, kernel, code, monkeypatch):
         r = dec.decode_batch(Hz, syn, 0.06 / 3, 30, algo="MS", want_post=True, layer_ptr=lp, layer_rows=lr)
         if kernel.startswith("G"):
             nm = _lib.kernel_name(Hz, lp, lr, "MS")
-            dc = Hz.sum(1).max()
-            want = f"ms_layered_cc_kernel<{dc}>" if kernel == "G1" else f"ms_layered_kernel<{dc}, {kernel[1:2]}>"
-            assert nm == want, nm
+            assert nm == f"ms_layered_kernel<{Hz.sum(1).max()}, {kernel[1:]}>", nm
     finally:
         code_h._sched.clear()
     e, it, post, fl = oracle.decode_batch("MS", Hz, syn, 0.06 / 3, 30, lp, lr)
