@@ -642,8 +642,8 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
     QLDPC_TICK(5);
   }
   if constexpr (QLDPC_OSD_TIMING != 0) {
-    if (lane == 0 && wave < 2)
-      for (int k = 0; k < 6; ++k) atomicAdd(a.prof + 8 * wave + k, tp[k]);
+    if (lane == 0 && (wave == engine || wave == (engine ^ 1)))   // [0]: the engine wave, [1]: another
+      for (int k = 0; k < 6; ++k) atomicAdd(a.prof + 8 * (wave == engine ? 0 : 1) + k, tp[k]);
   }
 #undef QLDPC_TICK
   if (rank < a.rank) {                              // greedy loop runs past column n-1

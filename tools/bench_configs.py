@@ -145,6 +145,13 @@ def main():
         ("LP118_2", "MS", "F", None, 50, S),
         ("LP118_2", "BP", "L", 0.05, 100, S // 2),           # configs[4] (decoder part)
     ]
+    if "--hbm-large" in sys.argv:
+        # batches that fill the chip: the kernel keeps min(batch, 16 waves per
+        # CU, 64 GB of state) slots resident (capi.cpp decode_hbm)
+        for pt in [(16384, 3, 6, "MS", None, 20, 196608), (16384, 3, 6, "MS", 0.02, 50, 262144),
+                   (16384, 3, 6, "BP", None, 10, 98304)]:
+            print(json.dumps(run_hbm(*pt)), flush=True)
+        return
     if "--hbm" in sys.argv:
         for pt in [(16384, 3, 6, "MS", None, 50, 16384), (16384, 3, 6, "MS", 0.02, 50, 65536),
                    (16384, 3, 6, "BP", None, 20, 8192), (None, None, None, "MS", None, 50, 65536, "LP118_0")]:
