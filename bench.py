@@ -38,6 +38,7 @@ import glob
 import hashlib
 import json
 import os
+import re
 import socket
 import struct
 import sys
@@ -124,19 +125,95 @@ def device_code_sha(path):
     return hashlib.sha256(data).hexdigest()
 
 
-def find_profile(kernel, sha):
+def _demangle_kernel(sym):
+    """'_ZN5qldpc15ms_flood_kernelILi8ELi4EEEvNS_10DecodeArgsE' -> 'ms_flood_kernel<8, 4>'
+    (the kernel names rocprofv3 prints for this library's templates: int and
+    bool non-type arguments only); None for anything else."""
+    m = re.match(r"_ZN5qldpc(\d+)", sym)
+    if not m:
+        return None
+    i = m.end()
+    name = sym[i:i + int(m.group(1))]
+    i += int(m.group(1))
+    if sym[i:i + 1] != "I":
+        return None
+    i += 1
+    args = []
+    while True:
+        a = re.compile(r"L([ib])(n?\d+)E").match(sym, i)
+        if not a:
+            break
+        args.append(("false", "true")[int(a.group(2))] if a.group(1) == "b" else a.group(2).replace("n", "-"))
+        i = a.end()
+    if sym[i:i + 1] != "E":
+        return None
+    return f"{name}<{', '.join(args)}>"
+
+
+def kernel_code_sha(path, kernel):
+    """sha256 of one kernel's machine code and kernel descriptor inside the
+    library's gfx950 code objects (every offload bundle of .hip_fatbin), so a
+    profile stays valid across edits of OTHER kernels; None if not found."""
+    with open(path, "rb") as f:
+        data = f.read()
+    h = None
+    pos = 0
+    while True:
+        pos = data.find(b"__CLANG_OFFLOAD_BUNDLE__", pos)
+        if pos < 0:
+            break
+        n_ent, = struct.unpack_from("<Q", data, pos + 24)
+        off = pos + 32
+        for _ in range(n_ent):
+            eo, esz, tl = struct.unpack_from("<QQQ", data, off)
+            triple = data[off + 24:off + 24 + tl]
+            off += 24 + tl
+            if b"gfx950" not in triple or esz == 0:
+                continue
+            elf = data[pos + eo:pos + eo + esz]
+            shoff, = struct.unpack_from("<Q", elf, 0x28)
+            shentsize, shnum, _ = struct.unpack_from("<HHH", elf, 0x3A)
+            secs = [struct.unpack_from("<IIQQQQIIQQ", elf, shoff + i * shentsize) for i in range(shnum)]
+            for s in secs:
+                if s[1] != 2:                                  # SHT_SYMTAB
+                    continue
+                strtab = secs[s[6]]
+                for j in range(s[5] // 24):
+                    st_name, st_info, _, st_shndx, st_value, st_size = struct.unpack_from("<IBBHQQ", elf, s[4] + j * 24)
+                    nm = elf[strtab[4] + st_name:elf.index(b"\0", strtab[4] + st_name)].decode()
+                    if (st_info & 0xf) != 2 or _demangle_kernel(nm) != kernel:     # STT_FUNC
+                        continue
+                    h = hashlib.sha256()
+                    tsec = secs[st_shndx]
+                    h.update(elf[tsec[4] + st_value - tsec[3]:tsec[4] + st_value - tsec[3] + st_size])
+                    for k in range(s[5] // 24):                # its kernel descriptor (<sym>.kd)
+                        kn, _, _, ksh, kv, ksz = struct.unpack_from("<IBBHQQ", elf, s[4] + k * 24)
+                        if elf[strtab[4] + kn:elf.index(b"\0", strtab[4] + kn)] == (nm + ".kd").encode():
+                            ks = secs[ksh]
+                            h.update(elf[ks[4] + kv - ks[3]:ks[4] + kv - ks[3] + ksz])
+                    return h.hexdigest()
+        pos += 24
+    return None
+
+
+def find_profile(kernel, sha, code_sha=None):
     """Newest profiles/*_roofline.json entry for this kernel built from this
-    device code (None if the committed profiles are stale for this build)."""
+    device code: the kernel's own machine-code hash (`code_sha256` of the
+    entry) when both sides have it, else the whole device image's (None if the
+    committed profiles are stale for this build)."""
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_roofline.json")), reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        if d.get("device_code_sha256") != sha:
-            continue
         for k in d.get("kernels", []):
-            if k.get("kernel") == kernel:
+            if k.get("kernel") != kernel:
+                continue
+            if code_sha is not None and k.get("code_sha256") is not None:
+                if k["code_sha256"] == code_sha:
+                    return os.path.relpath(path, ROOT), k
+            elif d.get("device_code_sha256") == sha:
                 return os.path.relpath(path, ROOT), k
     return None, None
 
@@ -418,7 +495,8 @@ def roofline(names, t_launch, hs_launch, it_launch, algo_launch, launches):
     from qldpcsim_amd import _lib
     kernel = names[0]
     sha = device_code_sha(_lib.LIB_PATH)
-    src, prof = find_profile(kernel, sha)
+    ksha = kernel_code_sha(_lib.LIB_PATH, kernel)
+    src, prof = find_profile(kernel, sha, ksha)
     r = {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
          "kernel": kernel, "kernel_ms_per_launch": t_launch * 1e3, "launches": launches,
          "units_per_launch": {"half_shots": hs_launch, "half_shot_iterations": it_launch},
@@ -430,7 +508,7 @@ def roofline(names, t_launch, hs_launch, it_launch, algo_launch, launches):
                                       "an HBM-streaming design's bytes, "
                                       "not what this LDS-resident kernel moves",
                  "peak_gbs": HBM_PEAK_GBS},
-         "device_code_sha256": sha, "profile": src}
+         "device_code_sha256": sha, "kernel_code_sha256": ksha, "profile": src}
     if prof is None:
         r["note"] = ("no counter profile under profiles/ for this kernel build "
                      "(tools/gpu_profile_roofline.sh regenerates it): bound and frac unmeasured")

@@ -85,7 +85,9 @@ def summarise_config(d):
             continue
         per_it = lambda n: c[n][0] / c[n][2]            # noqa: E731
         per_hs = lambda n: c[n][0] / c[n][1]            # noqa: E731
-        ent = {"kernel": k, **meta,
+        import bench
+        from qldpcsim_amd import _lib
+        ent = {"kernel": k, **meta, "code_sha256": bench.kernel_code_sha(_lib.LIB_PATH, k),
                "per_half_shot_iteration": {
                    "valu_insts": per_it("SQ_INSTS_VALU"),
                    "lds_cycles": per_it("SQ_LDS_IDX_ACTIVE"),
