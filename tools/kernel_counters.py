@@ -26,7 +26,10 @@ sys.path.insert(0, ROOT)
 
 def short(name):
     """'void qldpc::osd_block_kernel<17, 8, 2>(qldpc::OsdArgs)' -> 'osd_block_kernel<17, 8, 2>'."""
-    m = re.search(r"qldpc::([A-Za-z0-9_]+<[^()]*>|[A-Za-z0-9_]+)\(", name)
+    m = re.search(r"qldpc::(?:\(anonymous namespace\)::)?([A-Za-z0-9_]+<[^()]*>|[A-Za-z0-9_]+)\(", name)
+    if m:
+        return m.group(1)
+    m = re.match(r"(?:void )?([A-Za-z0-9_:]+)", name)          # library kernels: the qualified name only
     return m.group(1) if m else name
 
 
