@@ -827,9 +827,10 @@ static int choose_path(qldpc_schedule* s, int algo, LaunchCfg** cfg, bool* hbm) 
 
 static void record_timing(hipEvent_t e0, hipEvent_t e1);
 
-// The HBM-resident decode: slots = min(batch, 16 waves per CU, what a 64 GiB
-// (or half the free memory) workspace holds); the workspace belongs to the
-// schedule and an event orders launches that share it.
+// The HBM-resident decode: tiles of 64 half-shot slots, one workgroup each,
+// tiles = min(what the batch fills, the workgroups a CU holds at the kernel's
+// register use, what a 64 GiB (or half the free memory) workspace holds); the workspace belongs to the schedule and an event
+// orders launches that share it.
 static int decode_hbm(const qldpc_code* code, qldpc_schedule* s, int algo, const void* d_syn, int syn_format,
                       int64_t batch, double p, int max_iter, double beta, double eps, void* d_ehat,
                       int ehat_format, int32_t* d_iters, double* d_post, int32_t* d_flags, hipStream_t st) {
@@ -839,18 +840,20 @@ static int decode_hbm(const qldpc_code* code, qldpc_schedule* s, int algo, const
   int dev = 0, cus = 0;
   HIP_TRY(hipGetDevice(&dev));
   HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  const size_t w = algo == QLDPC_ALGO_MS ? 4 : 8;
-  const size_t per_slot = (size_t)code->E * w + (size_t)code->n * 8 + (size_t)code->m + 64;
+  const size_t w = algo == QLDPC_ALGO_MS ? 4 : 8;   // message / posterior row element (MS: f32 S)
+  const size_t per_tile = ((size_t)code->E * w + (size_t)code->n * w + (size_t)code->m) * 64;
   std::lock_guard<std::mutex> lk(s->mu);
   size_t free_b = 0, total_b = 0;
   HIP_TRY(hipMemGetInfo(&free_b, &total_b));
   const size_t budget = std::min<size_t>(free_b / 2 + s->hbm_ws_bytes, (size_t)64 << 30);
-  int64_t T = std::min<int64_t>((batch + 255) / 256 * 256, (int64_t)cus * 16 * 64);
-  T = std::min<int64_t>(T, (int64_t)(budget / per_slot) / 256 * 256);
-  if (T < 256) return fail(QLDPC_EUNSUP, "HBM decode needs %zu B per half-shot slot: device memory too small", per_slot);
-  const size_t off_post = (size_t)T * code->E * w;
-  const size_t off_syn = off_post + (size_t)T * code->n * 8;
-  const size_t need = off_syn + (size_t)T * code->m + 256;
+  int per_cu = 0;
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * qldpc::kHbmWaves, 0));
+  int64_t tiles = std::min<int64_t>((batch + 63) / 64, (int64_t)cus * std::max(per_cu, 1));
+  tiles = std::min<int64_t>(tiles, (int64_t)(budget / per_tile));
+  if (tiles < 1) return fail(QLDPC_EUNSUP, "HBM decode needs %zu B per 64-slot tile: device memory too small", per_tile);
+  const size_t off_post = ((size_t)tiles * code->E * w * 64 + 255) & ~(size_t)255;
+  const size_t off_syn = (off_post + (size_t)tiles * code->n * w * 64 + 255) & ~(size_t)255;
+  const size_t need = off_syn + (size_t)tiles * code->m * 64 + 256;
   if (!s->hbm_ev) HIP_TRY(hipEventCreateWithFlags(&s->hbm_ev, hipEventDisableTiming));
   if (need > s->hbm_ws_bytes) {
     if (s->hbm_ws) {
@@ -881,9 +884,8 @@ static int decode_hbm(const qldpc_code* code, qldpc_schedule* s, int algo, const
   a.n = code->n;
   a.E = code->E;
   a.c2v = s->hbm_ws;
-  a.post = (double*)((char*)s->hbm_ws + off_post);
+  a.post = (char*)s->hbm_ws + off_post;
   a.synT = (uint8_t*)s->hbm_ws + off_syn;
-  a.T = T;
   a.syn = (const uint8_t*)d_syn;
   a.ehat = (uint8_t*)d_ehat;
   a.iters = d_iters;
@@ -912,7 +914,7 @@ static int decode_hbm(const qldpc_code* code, qldpc_schedule* s, int algo, const
     HIP_TRY(hipEventCreate(&e1));
     HIP_TRY(hipEventRecord(e0, st));
   }
-  HIP_TRY(qldpc::launch_hbm(kern, a, (int)(T / 256), 256, s->d_h_fl_var, s->d_h_fl_pos, s->hbm_lazy ? 1 : 0, st));
+  HIP_TRY(qldpc::launch_hbm(kern, a, (int)tiles, s->d_h_fl_var, s->d_h_fl_pos, s->hbm_lazy ? 1 : 0, st));
   if (timed) {
     HIP_TRY(hipEventRecord(e1, st));
     record_timing(e0, e1);

@@ -6,10 +6,11 @@
 
 namespace qldpc {
 
-// One thread = one half-shot slot; every lane of a wave walks the same check /
-// variable at the same time, so graph reads are wave-uniform (scalar loads)
-// and message reads are coalesced: state is slot-major, element i of slot s at
-// i * T + s (T = slots in the grid).
+// One workgroup of kHbmWaves waves = one tile of 64 half-shot slots (lane l =
+// slot l); every lane of a wave walks the same check / variable at the same
+// time, so graph reads are wave-uniform (scalar loads) and message reads are
+// coalesced: tile g's element i of slot l at [g][i][64].
+constexpr int kHbmWaves = 4;   // (kernel names below spell it out)
 struct HbmArgs {
   // graph (relabeled variables, int32, global)
   const int32_t* row_ptr;   // [m+1] CSR
@@ -27,11 +28,10 @@ struct HbmArgs {
   const int32_t* adj_vars;  // [*]   relabeled variables adjacent to the layer's rows, ascending
   int n_layers;
   int m, n, E;
-  // workspace (slot-major)
-  void* c2v;                // [E][T]  float (MS) / double (BP)
-  double* post;             // [n][T]
-  uint8_t* synT;            // [m][T]
-  long long T;
+  // workspace (tile-major: [tiles][elements][64 slots])
+  void* c2v;                // [tiles][E][64]  float (MS) / double (BP)
+  void* post;               // [tiles][n][64]  float32 column sum S (MS) / float64 posterior (BP)
+  uint8_t* synT;            // [tiles][m][64]
   // batch
   const uint8_t* syn;       // [batch][m] bytes, or uint64 [batch][wm] words
   uint8_t* ehat;            // [batch][n] bytes, or uint64 [batch][wn] words
@@ -50,7 +50,7 @@ struct HbmArgs {
 const void* select_hbm_kernel(int algo, int dcmax, const char** name);
 // fl_var / fl_pos: first layer reaching each variable / CSC position; lazy =
 // the layers partition the rows (no state initialisation pass)
-hipError_t launch_hbm(const void* kernel, const HbmArgs& a, int grid, int block, const int32_t* fl_var,
-                      const int32_t* fl_pos, int lazy, hipStream_t stream);
+hipError_t launch_hbm(const void* kernel, const HbmArgs& a, int tiles, const int32_t* fl_var, const int32_t* fl_pos,
+                      int lazy, hipStream_t stream);
 
 }  // namespace qldpc

@@ -60,7 +60,7 @@ def test_large_code_takes_hbm_kernel_and_equals_oracle(algo, sched):
     H = _regular_code(12000, 3, 6, 1)
     layers = [np.arange(H.shape[0])] if sched == "F" else schedule.layerize(H)
     lp, lr = schedule.pack_layers(layers, H.shape[0])
-    assert _lib.kernel_name(H, lp, lr, algo).startswith("hbm_decode_kernel<")
+    assert _lib.kernel_name(H, lp, lr, algo).startswith("hbm_tile_kernel<")
     syn = np.concatenate([_syndromes(H, 40, 0.03, 2), np.random.default_rng(3).integers(0, 2, (8, H.shape[0]),
                                                                                         dtype=np.uint8)])
     _check(H, syn, algo, 0.03, 12 if algo == "BP" else 25, lp, lr)
@@ -76,7 +76,7 @@ def test_code_past_16_bit_tables_decodes():
     H = np.zeros((m, n), np.uint8)
     H[rng.permutation(np.repeat(np.arange(m), n // m)), np.arange(n)] = 1
     assert _lib.kernel_name(H, np.array([0, m], np.int32), np.arange(m, dtype=np.int32), "MS") \
-        .startswith("hbm_decode_kernel<0, 64>")
+        .startswith("hbm_tile_kernel<0, 64, 4>")
     syn = _syndromes(H, 24, 0.002, 5)
     _check(H, syn, "MS", 0.002, 10, bits=True)
 
@@ -94,7 +94,7 @@ def test_forced_hbm_matches_reference_goldens(algo, monkeypatch):
         if "raises" in c or c["algo"] != algo or c["code"] not in ("LP04_0", "LP118_0", "LP118_2", "steane"):
             continue
         H = half_matrix(c)
-        assert _lib.kernel_name(H, a["layer_ptr"], a["layer_rows"], algo).startswith("hbm_decode_kernel<")
+        assert _lib.kernel_name(H, a["layer_ptr"], a["layer_rows"], algo).startswith("hbm_tile_kernel<")
         r = decoders.decode_batch(H, torch.as_tensor(a["syn"], device="cuda"), c["p_phys"] / 3, c["max_iter"],
                                   algo=algo, want_post=True, layer_ptr=a["layer_ptr"], layer_rows=a["layer_rows"])
         torch.cuda.synchronize()
@@ -121,7 +121,7 @@ def test_forced_hbm_early_stopping_batch_equals_lds_kernels(monkeypatch):
     s = torch.as_tensor(syn, device="cuda")
     ref = decoders.decode_batch(Hz, s, 0.04 / 3, 40, algo="MS", want_post=True, layer_ptr=lp, layer_rows=lr)
     monkeypatch.setenv("QLDPC_FORCE_HBM", "1")
-    assert _lib.kernel_name(Hz, lp, lr, "MS") == "hbm_decode_kernel<0, 8>"
+    assert _lib.kernel_name(Hz, lp, lr, "MS") == "hbm_tile_kernel<0, 8, 4>"
     got = decoders.decode_batch(Hz, s, 0.04 / 3, 40, algo="MS", want_post=True, layer_ptr=lp, layer_rows=lr)
     torch.cuda.synchronize()
     assert torch.equal(got.iters, ref.iters) and torch.equal(got.ehat, ref.ehat)
