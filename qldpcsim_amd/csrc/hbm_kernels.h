@@ -10,7 +10,10 @@ namespace qldpc {
 // slot l); every lane of a wave walks the same check / variable at the same
 // time, so graph reads are wave-uniform (scalar loads) and message reads are
 // coalesced: tile g's element i of slot l at [g][i][64].
-constexpr int kHbmWaves = 4;   // (kernel names below spell it out)
+#ifndef QLDPC_HBM_WAVES
+#define QLDPC_HBM_WAVES 4
+#endif
+constexpr int kHbmWaves = QLDPC_HBM_WAVES;   // (kernel names in hbm_kernels.hip spell out 4)
 struct HbmArgs {
   // graph (relabeled variables, int32, global)
   const int32_t* row_ptr;   // [m+1] CSR

@@ -95,7 +95,10 @@ __global__ void __launch_bounds__(64 * W) hbm_tile_kernel(HbmArgs a, const int32
                                                         const int32_t* __restrict__ fl_pos, int lazy) {
   using Msg = typename std::conditional<ALGO == ALGO_MS, float, double>::type;
   using Post = Msg;                                 // MS: float32 column sum S; BP: float64 posterior
-  constexpr int UC = DCMAX <= 8 ? 2 : 1;           // checks per load batch
+#ifndef QLDPC_HBM_UC
+#define QLDPC_HBM_UC 1
+#endif
+  constexpr int UC = QLDPC_HBM_UC;                   // checks per load step (1: 16 waves per CU; 2: 12, 4: 8 — slower, r03o)
   constexpr int UV = 4, KV = 8;                   // variables per load batch, messages loaded up front
   __shared__ uint32_t xb[3][W * 64];              // per-wave partials: [0] filters / flags, [1] stop test, [2] B
   __shared__ long long shot_s[64];

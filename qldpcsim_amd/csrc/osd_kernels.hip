@@ -315,15 +315,21 @@ __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL]
            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pivm);
     // next column with a pivot: the search loop only reads the state, so
     // skipping dependent columns costs no register copies at the joins
+    // Slots are scanned in ascending order and the scan stops at the first
+    // hit (uniform branches): once rows fill up, slot 0 almost always holds
+    // the pivot; a select chain over all SF slots cost 7 instructions each.
     int f = 0x7fffffff, bit = 0;
     while (cols) {
       bit = (int)__builtin_ctz(cols);
       cols &= cols - 1;
       const uint32_t bm = 1u << bit;
 #pragma unroll
-      for (int s = SF - 1; s >= 0; --s) {
+      for (int s = 0; s < SF; ++s) {
         const uint64_t c = __ballot(((HI ? hi[s] : lo[s]) & bm) != 0) & fm[s];
-        f = c ? 64 * s + (int)__builtin_ctzll(c) : f;
+        if (c) {
+          f = 64 * s + (int)__builtin_ctzll(c);
+          break;
+        }
       }
       f = __builtin_amdgcn_readfirstlane(f);
       if (f != 0x7fffffff) break;                   // (dependent columns: not in J)
@@ -354,8 +360,8 @@ __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL]
 #pragma unroll
     for (int s = 0; s < SF; ++s) {
       if (((HI ? hi[s] : lo[s]) & bm) != 0 && (s != fs || notme)) {   // rows holding a 1,
-        lo[s] ^= plo;                                                  // above and below
-        hi[s] ^= phi;
+        if (!HI) lo[s] ^= plo;                                         // above and below (the
+        hi[s] ^= phi;                                                  // low half is done in HI)
         cl[s] ^= pcl;
         ch[s] ^= pch;
       }
