@@ -34,7 +34,7 @@ from .schedule import pack_layers
 __all__ = ["MS_decoder", "BP_decoder", "OSDdec", "decode_batch", "DecodeResult", "osd_perm", "pack_bits",
            "unpack_bits",
            "osd_perms", "apply_osd", "apply_osd_device", "apply_osd_device_many", "osd_device_stage",
-           "osd_device_finish", "osd_status_check"]
+           "osd_device_finish", "osd_host_orders", "osd_status_check"]
 
 
 @dataclass
@@ -383,54 +383,93 @@ def _device_buf(key, shape, dtype, dev):
     return buf[:need].view(shape)
 
 
-def osd_device_finish(items, staged, order, stream=None):
-    """Second half: for each staged decode (waiting only for its own event),
-    the shots the device order could not decide (status 2) get NumPy's
-    reliability order on the host (their posteriors only, pinned copies) and
-    the GPU elimination; then the corrected estimates are scattered back, all
-    queued asynchronously. res.osd_status keeps 0 / 1 per shot (1: the
-    reference's IndexError case, raised by osd_status_check)."""
+def osd_device_finish(items, staged, order, stream=None, host=None):
+    """Second half: for each staged decode, the shots the device order could
+    not decide (status 2) get NumPy's reliability order on the host (their
+    posteriors only, pinned copies) and the GPU elimination; then the
+    corrected estimates are scattered back, all queued asynchronously.
+    `host` = the result of osd_host_orders(staged) if the caller already ran
+    it (e.g. on a worker thread while the GPU ran the next batch); otherwise
+    it runs here. res.osd_status keeps 0 / 1 per shot (1: the reference's
+    IndexError case, raised by osd_status_check)."""
+    if host is None:
+        host = osd_host_orders(staged)
     with _on_stream(stream):
-        for (H, syn, res), sg in zip(items, staged):
+        for (H, syn, res), sg, hr in zip(items, staged, host):
             if sg is not None:
-                _osd_finish_one(H, syn, res, sg, order)
+                _osd_finish_device(H, syn, res, sg, hr, order)
     return staged
 
 
-def _osd_finish_one(H, syn, res, sg, order):
+def osd_host_orders(staged):
+    """The host part of osd_device_finish, for every staged decode: wait for
+    its device OSD (its event only), fetch the status-2 shots' posteriors and
+    compute NumPy's reliability orders (decoders.py:320-325) for all of them
+    in one pass over the host threads. Blocking, touches no launch stream, so
+    a pipelined caller runs it on a worker thread while the GPU decodes the
+    next batch. Returns per decode None (no staging) or (redo, perms_pinned)."""
     import torch
-    bad, post_b, syn_b, e_b, status, status_h, ev, slot, _, spill = sg
-    dev = res.ehat.device
-    code = _lib.code_for(H, dev.index)
-    ev.synchronize()
-    redo = (status_h.numpy() == 2).nonzero()[0]
-    res.osd_host_order = int(redo.size)
-    if redo.size:
+    out, blocks = [], []
+    for sg in staged:
+        if sg is None:
+            out.append(None)
+            continue
+        bad, post_b, syn_b, e_b, status, status_h, ev, slot, _, spill = sg
+        dev = post_b.device
+        ev.synchronize()
+        redo = (status_h.numpy() == 2).nonzero()[0]
+        if redo.size == 0:
+            out.append((redo, None))
+            continue
         k2 = int(redo.size)
-        host = _pinned(("post", slot), (k2, post_b.shape[1]), torch.float64)
-        # fetch these posteriors with copies that wait only for this
-        # decode's OSD (its event), on a side stream, so the launch stream's
-        # next batch (decode, device OSD) runs during the host's NumPy order
+        hostp = _pinned(("post", slot), (k2, post_b.shape[1]), torch.float64)
+        # fetch these posteriors on a side stream, with copies that wait only
+        # for this decode's OSD (its event): the launch stream's next batch
+        # (decode, device OSD) keeps running
         side = _side_stream(dev)
         side.wait_event(ev)
         if spill is not None and k2 <= spill[3] and int(spill[2][0]) == k2:
-            # the kernels spilled exactly these rows: one contiguous DMA
-            # copy (no gather kernel waiting for free CUs behind other work)
+            # the kernels spilled exactly these rows: one contiguous DMA copy
+            # (no gather kernel waiting for free CUs behind other work)
             sp_post, sp_idx, _, _ = spill
             idx_h = _pinned(("spill_idx", slot), (k2,), torch.int32)
             with torch.cuda.stream(side):
-                host.copy_(sp_post[:k2], non_blocking=True)
+                hostp.copy_(sp_post[:k2], non_blocking=True)
                 idx_h.copy_(sp_idx[:k2], non_blocking=True)
             side.synchronize()
             redo = idx_h.numpy().astype(np.int64)
         else:
             with torch.cuda.stream(side):
                 idx_s = torch.as_tensor(redo, device=dev)
-                host.copy_(post_b.index_select(0, idx_s), non_blocking=True)
+                hostp.copy_(post_b.index_select(0, idx_s), non_blocking=True)
             side.synchronize()
+        out.append((redo, _pinned(("perm", slot), (k2, post_b.shape[1]), torch.int32)))
+        blocks.append((len(out) - 1, hostp.numpy()))
+    if blocks:
+        # every decode's rows in one threaded pass (better parallel efficiency
+        # than one pass per decode)
+        if len(blocks) == 1 or len({b.shape[1] for _, b in blocks}) > 1:
+            for i, P in blocks:
+                out[i][1].numpy()[...] = osd_perms(P)
+        else:
+            perms = osd_perms(np.concatenate([P for _, P in blocks]))
+            r0 = 0
+            for i, P in blocks:
+                out[i][1].numpy()[...] = perms[r0:r0 + P.shape[0]]
+                r0 += P.shape[0]
+    return out
+
+
+def _osd_finish_device(H, syn, res, sg, hr, order):
+    import torch
+    bad, post_b, syn_b, e_b, status, status_h, ev, slot, _, spill = sg
+    dev = res.ehat.device
+    code = _lib.code_for(H, dev.index)
+    redo, perm_h = hr
+    res.osd_host_order = int(redo.size)
+    if redo.size:
+        k2 = int(redo.size)
         idx = torch.as_tensor(redo, device=dev)
-        perm_h = _pinned(("perm", slot), (k2, post_b.shape[1]), torch.int32)
-        perm_h.numpy()[...] = osd_perms(host.numpy())
         perms = perm_h.to(dev, non_blocking=True)
         syn_r = syn_b.index_select(0, idx)
         e_r = e_b.index_select(0, idx)

@@ -213,6 +213,19 @@ def _dist():
     return None, 0, 1
 
 
+_WORKER = []
+
+
+def _host_worker():
+    """One background thread for the pipelined OSD's host work (waiting for a
+    batch's device OSD, fetching the status-2 posteriors, NumPy's orders), so
+    the main thread keeps queueing the next batch's GPU work."""
+    from concurrent.futures import ThreadPoolExecutor
+    if not _WORKER:
+        _WORKER.append(ThreadPoolExecutor(1))
+    return _WORKER[0]
+
+
 def simulate_p(Hx: np.ndarray, Hz: np.ndarray, p: float, shots: int = 1000, decType: str = "MS",
                decIterations: int = 99, decSchedule: str = "F", OSDorder: int = -1,
                rngSeed: Optional[int] = None, *, batch_size: Optional[int] = None,
@@ -299,22 +312,25 @@ def simulate_p(Hx: np.ndarray, Hz: np.ndarray, p: float, shots: int = 1000, decT
             if cur is not None and osd >= 0 and stage_first:
                 # many OSD shots: this batch's device OSD is queued first
                 # (staging waits for its decode), so the GPU runs it while the
-                # host finishes the previous batch's NumPy orders below
+                # worker thread finishes the previous batch's NumPy orders
                 cur[6] = decoders.osd_device_stage([(Hz, cur[0], cur[4]), (Hx, cur[1], cur[5])],
                                                    slot0=2 * phase, order=osd)
+                cur.append(_host_worker().submit(decoders.osd_host_orders, cur[6]))
                 phase ^= 1
             if pending is not None:
-                sy_z_, sy_x_, errX_, errZ_, rX_, rZ_, staged = pending
+                sy_z_, sy_x_, errX_, errZ_, rX_, rZ_, staged = pending[:7]
                 items = [(Hz, sy_z_, rX_), (Hx, sy_x_, rZ_)]
                 if osd >= 0:                           # (decoders.py:179-180), on the GPU
-                    decoders.osd_device_finish(items, staged, osd)
+                    # the status-2 shots' NumPy orders were computed on the
+                    # worker thread while the GPU decoded this batch
+                    decoders.osd_device_finish(items, staged, osd, host=pending[7].result())
                     decoders.osd_status_check(items, defer=osd_flags)
                 ch.count_device(sy_z_, sy_x_, errX_, errZ_, rX_.ehat, rZ_.ehat, rX_.iters, rZ_.iters, acc)
             if cur is not None and osd >= 0 and cur[6] is None:
-                # few OSD shots: the host's orders for the previous batch ran
-                # during this batch's decode; stage (and sync on) it now
+                # few OSD shots: stage (and sync on) this batch's decode now
                 cur[6] = decoders.osd_device_stage([(Hz, cur[0], cur[4]), (Hx, cur[1], cur[5])],
                                                    slot0=2 * phase, order=osd)
+                cur.append(_host_worker().submit(decoders.osd_host_orders, cur[6]))
                 phase ^= 1
             if cur is not None and osd >= 0:
                 stage_first = decoders.osd_staged_on_device(cur[6])
