@@ -74,6 +74,8 @@ def parse(argv=None):
                     help="syndrome / hard-decision format in HBM: bit-packed 64-bit words (default) or bytes")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="bounded CPU-baseline sample per leg (0 disables)")
+    ap.add_argument("--hbm-leg", type=int, default=1,
+                    help="N=1: also time the same workload through the HBM-resident kernel (hbm_streaming field)")
     ap.add_argument("--worklog", default=None,
                     help="write per-launch work (kernel, half-shots, iterations) as JSON (profiling)")
     return ap.parse_args(argv)
@@ -451,6 +453,10 @@ def run_rank(args, rank, world, local):
     algo_launch = algo_bytes * it_per_launch + io_bytes * hs_per_launch
     roof = roofline(names, avg_launch_s, hs_per_launch, it_per_launch, algo_launch, launches)
 
+    hbm_leg = None
+    if world == 1 and args.hbm_leg and not args.worklog:
+        hbm_leg = hbm_streaming_leg(halves, outs, prior, args, B, bits, algo_launch, dev)
+
     sched_name = {"F": "flooding", "L": "layered", "S": "serial"}[args.schedule]
     algo_name = "normalized min-sum (beta 0.75)" if args.algo == "MS" else "sum-product BP"
     synd = "fixed-work uniform random syndromes (SURVEY.md 8d(i))" if args.p is None else \
@@ -481,12 +487,53 @@ def run_rank(args, rank, world, local):
         },
         "roofline": roof,
     }
+    if hbm_leg is not None:
+        out["hbm_streaming"] = hbm_leg
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def hbm_streaming_leg(halves, outs, prior, args, B, bits, algo_launch, dev, steps=2):
+    """The same workload through hbm_tile_kernel (message state in HBM, every
+    message a coalesced 256-byte tile row; QLDPC_FORCE_HBM=1): SURVEY.md
+    §8(d)'s HBM roofline is the bound of that design. Reported beside the
+    headline (which is the LDS-resident kernel's), untimed by the headline."""
+    import torch
+    from qldpcsim_amd import _lib, decoders
+    os.environ["QLDPC_FORCE_HBM"] = "1"
+    try:
+        name = _lib.kernel_name(halves[0][0], halves[0][2], halves[0][3], args.algo, dev.index)
+
+        def step():
+            for (H, s, lp, lr), o in zip(halves, outs):
+                decoders.decode_batch(H, s, prior, args.iters, algo=args.algo, out=o, layer_ptr=lp,
+                                      layer_rows=lr, want_post=False, ehat_bits=bits)
+        step()
+        torch.cuda.synchronize()
+        _lib.timing_enable(True)
+        _lib.timing_reset()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        kern_ms, launches = _lib.timing_read()
+        _lib.timing_enable(False)
+    finally:
+        os.environ.pop("QLDPC_FORCE_HBM", None)
+    t_launch = kern_ms / 1e3 / launches
+    gbs = algo_launch / t_launch / 1e9
+    return {"kernel": name, "value": B * steps / el, "unit": "shots/s", "steps": steps,
+            "kernel_ms_per_launch": t_launch * 1e3, "algorithmic_gbs": gbs, "peak_gbs": HBM_PEAK_GBS,
+            "frac": gbs / HBM_PEAK_GBS,
+            "note": "the same workload and iteration counts through the HBM-resident decoder "
+                    "(QLDPC_FORCE_HBM=1); GB/s under SURVEY.md 8d's algorithmic model (the kernel moves "
+                    "about 1.27x those bytes: post and c2v rows both read per edge); the headline value is "
+                    "the LDS-resident kernel's"}
 
 
 def roofline(names, t_launch, hs_launch, it_launch, algo_launch, launches):

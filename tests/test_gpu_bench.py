@@ -47,6 +47,9 @@ def test_bench_single_gpu_line():
         ["qldpc_oracle.c,", "numpy_dense.py"]
     assert cb["reference_context"]["value"] == 2.61
     assert d["config"]["avg_iterations"] == 50.0
+    hs = d["hbm_streaming"]                         # the same workload on the HBM-resident kernel
+    assert hs["kernel"].startswith("hbm_tile_kernel<0, 8") and hs["value"] > 0
+    assert 0 < hs["frac"] < 1 and hs["peak_gbs"] == 8000.0
 
 
 def test_bench_layered_channel_line():
