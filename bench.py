@@ -74,6 +74,8 @@ def parse(argv=None):
                     help="syndrome / hard-decision format in HBM: bit-packed 64-bit words (default) or bytes")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="bounded CPU-baseline sample per leg (0 disables)")
+    ap.add_argument("--path", default="auto", choices=["auto", "hbm"],
+                    help="hbm: decode through the HBM-resident kernel (QLDPC_FORCE_HBM=1) in the timed region")
     ap.add_argument("--hbm-leg", type=int, default=1,
                     help="N=1: also time the same workload through the HBM-resident kernel (hbm_streaming field)")
     ap.add_argument("--worklog", default=None,
@@ -363,6 +365,8 @@ def run_rank(args, rank, world, local):
         else:
             dist.init_process_group(backend)
 
+    if args.path == "hbm":
+        os.environ["QLDPC_FORCE_HBM"] = "1"
     from qldpcsim_amd import _lib, codes, decoders, schedule
     from qldpcsim_amd.simulator import DeviceChannel
     Hx, Hz = codes.load_code(args.code)
@@ -454,7 +458,7 @@ def run_rank(args, rank, world, local):
     roof = roofline(names, avg_launch_s, hs_per_launch, it_per_launch, algo_launch, launches)
 
     hbm_leg = None
-    if world == 1 and args.hbm_leg and not args.worklog:
+    if world == 1 and args.hbm_leg and not args.worklog and args.path != "hbm":
         hbm_leg = hbm_streaming_leg(halves, outs, prior, args, B, bits, algo_launch, dev)
 
     sched_name = {"F": "flooding", "L": "layered", "S": "serial"}[args.schedule]
@@ -527,7 +531,12 @@ def hbm_streaming_leg(halves, outs, prior, args, B, bits, algo_launch, dev, step
         os.environ.pop("QLDPC_FORCE_HBM", None)
     t_launch = kern_ms / 1e3 / launches
     gbs = algo_launch / t_launch / 1e9
+    measured = None
+    _, prof = find_profile(name, None, kernel_code_sha(_lib.LIB_PATH, name))
+    if prof is not None:                               # PMC bytes per half-shot of this kernel build
+        measured = prof["per_half_shot"]["hbm_bytes"] * (2 * B * steps / launches) / t_launch / 1e9
     return {"kernel": name, "value": B * steps / el, "unit": "shots/s", "steps": steps,
+            "measured_gbs": measured, "measured_frac": None if measured is None else measured / HBM_PEAK_GBS,
             "kernel_ms_per_launch": t_launch * 1e3, "algorithmic_gbs": gbs, "peak_gbs": HBM_PEAK_GBS,
             "frac": gbs / HBM_PEAK_GBS,
             "note": "the same workload and iteration counts through the HBM-resident decoder "
@@ -552,8 +561,10 @@ def roofline(names, t_launch, hs_launch, it_launch, algo_launch, launches):
                  "algorithmic_model": "SURVEY.md 8d: per executed half-shot iteration w(3E+2n) flooding "
                                       "(layered: sum_l w(2E_l + sum_{V_l} d_j + 2|V_l|)), w = 4 MS / 8 BP, "
                                       "+ I/O bytes per half-shot (m+n+4, or 8(ceil(m/64)+ceil(n/64))+4 bit-packed); "
-                                      "an HBM-streaming design's bytes, "
-                                      "not what this LDS-resident kernel moves",
+                                      + ("an HBM-streaming design's bytes, not what this LDS-resident kernel moves"
+                                         if not kernel.startswith("hbm_tile") else
+                                         "this HBM-resident kernel moves about 1.28x these bytes (post and c2v "
+                                         "rows both read per edge)"),
                  "peak_gbs": HBM_PEAK_GBS},
          "device_code_sha256": sha, "kernel_code_sha256": ksha, "profile": src}
     if prof is None:
@@ -578,11 +589,14 @@ def roofline(names, t_launch, hs_launch, it_launch, algo_launch, launches):
     lds = pu["lds_cycles"] * it_launch / t_launch / 1e9              # G LDS-array cycles / s (chip)
     lds_peak = CUS * CLOCK_GHZ
     traffic = prof["per_half_shot"]["hbm_bytes"] * hs_launch
+    hbm_gbs = traffic / t_launch / 1e9                                # measured (PMC) HBM bytes
     units = {"valu": {"achieved": valu, "peak": valu_peak, "unit": valu_unit,
                       "frac": valu / valu_peak,
                       "frac_lo": None if valu_lo is None else valu_lo / valu_peak},
              "lds": {"achieved": lds, "peak": lds_peak, "unit": "G LDS-array cycles/s (all CUs)",
-                     "frac": lds / lds_peak}}
+                     "frac": lds / lds_peak},
+             "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s (measured HBM bytes)",
+                     "frac": hbm_gbs / HBM_PEAK_GBS}}
     bound = max(units, key=lambda k: units[k]["frac"])
     r.update(bound=bound, achieved=units[bound]["achieved"], peak=units[bound]["peak"],
              unit=units[bound]["unit"], frac=units[bound]["frac"], traffic=traffic, units=units)
@@ -591,7 +605,8 @@ def roofline(names, t_launch, hs_launch, it_launch, algo_launch, launches):
                     "launch time), valu_cycles = 2 x SQ_INSTS_VALU + 2 x (ADD+MUL+FMA_F64) + 14 x TRANS_F64 + "
                     "6 x TRANS_F32 (per-class SQ_INSTS_VALU_* counters) + 2 x the unclassified rest "
                     "(float64 min/max/compare have no class counter; frac_lo leaves it out); lds frac = lds_cycles/half-shot-iter x "
-                    "iterations/launch / (256 CUs x 2.4 GHz x launch time); per-unit counts from the "
+                    "iterations/launch / (256 CUs x 2.4 GHz x launch time); hbm frac = PMC HBM bytes/half-shot x "
+                    "half-shots/launch / launch time / 8000 GB/s; bound = the largest; per-unit counts from the "
                     "profile (SQ_INSTS_VALU, SQ_LDS_IDX_ACTIVE; traffic = 2 x FETCH_SIZE + WRITE_SIZE), "
                     "launch time and iterations from this run")
     r["profile_clock_ghz"] = prof.get("clock_ghz")
