@@ -33,6 +33,26 @@ def test_host_cores_and_device_code_hash():
     assert len(h) == 64 and h == bench.device_code_sha(_lib.LIB_PATH)
 
 
+def test_kernel_code_hash_keys_committed_profiles():
+    """Each roofline profile entry is keyed by its own kernel's machine code:
+    the demangler maps the library's symbols to rocprofv3's kernel names, every
+    decode kernel bench.py can price has a hash, and distinct kernels differ."""
+    from qldpcsim_amd import _lib
+    assert bench._demangle_kernel("_ZN5qldpc15ms_flood_kernelILi8ELi4EEEvNS_10DecodeArgsE") == "ms_flood_kernel<8, 4>"
+    assert bench._demangle_kernel("_ZN5qldpc14bp_team_kernelILb0ELi8ELi4EEEvNS_10DecodeArgsE") == \
+        "bp_team_kernel<false, 8, 4>"
+    assert bench._demangle_kernel("_Z3foov") is None
+    names = ["ms_flood_kernel<8, 4>", "ms_layered_kernel<8, 1>", "bp_team_kernel<false, 8, 4>",
+             "bp_team_lg_kernel<8, 4>", "hbm_tile_kernel<0, 8, 4>", "hbm_tile_kernel<1, 8, 4>",
+             "osd_block_kernel<17, 8, 2>"]
+    hs = [bench.kernel_code_sha(_lib.LIB_PATH, k) for k in names]
+    assert all(h is not None and len(h) == 64 for h in hs) and len(set(hs)) == len(hs)
+    assert bench.kernel_code_sha(_lib.LIB_PATH, "no_such_kernel<1>") is None
+    # a profile entry is found only under its own hash
+    src, ent = bench.find_profile("ms_flood_kernel<8, 4>", None, "0" * 64)
+    assert src is None and ent is None
+
+
 def test_gpus_disagreeing_with_world_size_fails():
     env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "3"], cwd=ROOT, capture_output=True,

@@ -52,6 +52,21 @@ def test_bench_single_gpu_line():
     assert 0 < hs["frac"] < 1 and hs["peak_gbs"] == 8000.0
 
 
+def test_bench_hbm_path_line():
+    """--path hbm times the HBM-resident kernel as the main leg: same workload,
+    its roofline includes the measured-HBM unit (bound hbm when the committed
+    profile matches this build)."""
+    r = _bench("--path", "hbm", "--steps", "1", "--warmup", "1", "--batch", "65536", "--cpu-seconds", "0")
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    rf = d["roofline"]
+    assert rf["kernel"] == "hbm_tile_kernel<0, 8, 4>" and d["config"]["avg_iterations"] == 50.0
+    assert "hbm_streaming" not in d
+    if rf["profile"] is not None:
+        assert set(rf["units"]) == {"valu", "lds", "hbm"} and rf["bound"] == "hbm"
+        assert 0.05 < rf["frac"] <= 1.05
+
+
 def test_bench_layered_channel_line():
     r = _bench("--steps", "1", "--warmup", "1", "--batch", "16384", "--cpu-seconds", "0",
                "--code", "LP118_2", "--schedule", "L", "--p", "0.05")
