@@ -226,6 +226,14 @@ def _host_worker():
     return _WORKER[0]
 
 
+def _host_orders_on(dev, staged):
+    """decoders.osd_host_orders on the worker thread, with this rank's device
+    current there too (the HIP current device is per thread)."""
+    import torch
+    torch.cuda.set_device(dev)
+    return decoders.osd_host_orders(staged)
+
+
 def simulate_p(Hx: np.ndarray, Hz: np.ndarray, p: float, shots: int = 1000, decType: str = "MS",
                decIterations: int = 99, decSchedule: str = "F", OSDorder: int = -1,
                rngSeed: Optional[int] = None, *, batch_size: Optional[int] = None,
@@ -315,7 +323,7 @@ def simulate_p(Hx: np.ndarray, Hz: np.ndarray, p: float, shots: int = 1000, decT
                 # worker thread finishes the previous batch's NumPy orders
                 cur[6] = decoders.osd_device_stage([(Hz, cur[0], cur[4]), (Hx, cur[1], cur[5])],
                                                    slot0=2 * phase, order=osd)
-                cur.append(_host_worker().submit(decoders.osd_host_orders, cur[6]))
+                cur.append(_host_worker().submit(_host_orders_on, dev, cur[6]))
                 phase ^= 1
             if pending is not None:
                 sy_z_, sy_x_, errX_, errZ_, rX_, rZ_, staged = pending[:7]
@@ -330,7 +338,7 @@ def simulate_p(Hx: np.ndarray, Hz: np.ndarray, p: float, shots: int = 1000, decT
                 # few OSD shots: stage (and sync on) this batch's decode now
                 cur[6] = decoders.osd_device_stage([(Hz, cur[0], cur[4]), (Hx, cur[1], cur[5])],
                                                    slot0=2 * phase, order=osd)
-                cur.append(_host_worker().submit(decoders.osd_host_orders, cur[6]))
+                cur.append(_host_worker().submit(_host_orders_on, dev, cur[6]))
                 phase ^= 1
             if cur is not None and osd >= 0:
                 stage_first = decoders.osd_staged_on_device(cur[6])
