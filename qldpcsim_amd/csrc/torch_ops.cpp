@@ -1,0 +1,132 @@
+// torch_ops.cpp — the batched decoder as a PyTorch-ROCm C++ operator.
+//
+//   torch.ops.qldpc.decode(syndromes, H, layer_ptr, layer_rows, p, max_iter,
+//                          algo="MS", beta=0.75, eps=1e-9, want_post=False,
+//                          ehat_bits=False) -> (ehat, iters, post, flags)
+//
+// Replaces, per batch, the reference's per-shot MS_decoder / BP_decoder calls
+// (qLDPCsim/decoders.py:110-117, :189-195) for torch code: the HIP kernels of
+// libqldpc_hip.so behind the C ABI (include/qldpc_decoder.h), launched on
+// torch's current HIP stream of the syndromes' device, outputs allocated
+// through torch's caching allocator. The Tanner graph of H and each layer
+// partition are built once per (device, H) and cached here.
+//
+// Arguments: syndromes uint8 [B, m] (one byte per check) or int64
+// [B, ceil(m/64)] (bit-packed words) on a HIP device; H [m, n] and the
+// schedule (layer_ptr [L+1], layer_rows, int32 or int64) as CPU tensors.
+// Errors as decode_batch / the reference: ValueError for shapes / options
+// (and for CPU syndromes: there is no CPU path), IndexError for layer rows out
+// of range (decoders.py:156, :250), RuntimeError for HIP failures.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include <map>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <utility>
+#include <vector>
+
+#include "../../include/qldpc_decoder.h"
+
+namespace {
+
+struct CodeEntry {
+  qldpc_code* code = nullptr;
+  std::map<std::vector<int32_t>, qldpc_schedule*> scheds;   // key: layer_ptr ++ layer_rows
+};
+std::mutex g_mu;
+std::map<std::pair<int, std::string>, CodeEntry> g_codes;  // (device, shape + H bytes)
+
+void check(int rc) {
+  if (rc == QLDPC_OK) return;
+  const char* msg = qldpc_last_error();
+  TORCH_CHECK_VALUE(rc != QLDPC_EINVAL, "qldpc::decode: ", msg);
+  TORCH_CHECK_INDEX(rc != QLDPC_ERANGE, "qldpc::decode: ", msg);
+  TORCH_CHECK(false, "qldpc::decode: ", msg);
+}
+
+std::vector<int32_t> as_i32(const at::Tensor& t, const char* what) {
+  TORCH_CHECK_VALUE(t.device().is_cpu() && t.dim() == 1, "qldpc::decode: ", what, " must be a 1-D CPU tensor");
+  const at::Tensor c = t.to(at::kInt).contiguous();
+  return std::vector<int32_t>(c.data_ptr<int32_t>(), c.data_ptr<int32_t>() + c.numel());
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> decode_hip(
+    const at::Tensor& syn, const at::Tensor& H, const at::Tensor& layer_ptr, const at::Tensor& layer_rows,
+    double p, int64_t max_iter, c10::string_view algo, double beta, double eps, bool want_post, bool ehat_bits) {
+  const int a = algo == "MS" ? QLDPC_ALGO_MS : algo == "BP" ? QLDPC_ALGO_BP : -1;
+  TORCH_CHECK_VALUE(a >= 0, "Unrecognized decoder type.");
+  TORCH_CHECK_VALUE(max_iter >= 1, "max_iter must be >= 1");
+  TORCH_CHECK_VALUE(H.device().is_cpu() && H.dim() == 2, "qldpc::decode: H must be a 2-D CPU tensor");
+  const int64_t m = H.size(0), n = H.size(1);
+  TORCH_CHECK_VALUE(syn.dim() == 2, "qldpc::decode: syndromes must be [B, m] bytes or [B, ceil(m/64)] words");
+  const int64_t B = syn.size(0), wm = (m + 63) / 64, wn = (n + 63) / 64;
+  int fmt;
+  if (syn.scalar_type() == at::kByte && syn.size(1) == m) fmt = QLDPC_FMT_BYTES;
+  else if (syn.scalar_type() == at::kLong && syn.size(1) == wm) fmt = QLDPC_FMT_BITS;
+  else TORCH_CHECK_VALUE(false, "qldpc::decode: syndromes must be uint8 [B, ", m, "] or int64 words [B, ", wm, "]");
+  const at::Tensor s = syn.contiguous();
+  const c10::hip::HIPGuard guard(s.device());
+  const int dev = s.get_device();
+
+  // graph and schedule, built once per (device, H) / layer partition
+  const at::Tensor Hb = H.remainder(2).to(at::kByte).contiguous();          // load_matrix's (mat % 2)
+  std::string key(reinterpret_cast<const char*>(&m), sizeof m);
+  key.append(reinterpret_cast<const char*>(&n), sizeof n);
+  key.append(reinterpret_cast<const char*>(Hb.data_ptr<uint8_t>()), (size_t)(m * n));
+  std::vector<int32_t> lp = as_i32(layer_ptr, "layer_ptr"), lr = as_i32(layer_rows, "layer_rows");
+  TORCH_CHECK_VALUE(lp.size() >= 2 && lp.front() == 0 && (size_t)lp.back() == lr.size(),
+                    "qldpc::decode: layer_ptr must run from 0 to len(layer_rows)");
+  std::vector<int32_t> skey(lp);
+  skey.push_back(-1);
+  skey.insert(skey.end(), lr.begin(), lr.end());
+  qldpc_code* code = nullptr;
+  qldpc_schedule* sched = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    CodeEntry& ce = g_codes[{dev, key}];
+    if (!ce.code) check(qldpc_code_create(Hb.data_ptr<uint8_t>(), (int)m, (int)n, &ce.code));
+    code = ce.code;
+    auto it = ce.scheds.find(skey);
+    if (it == ce.scheds.end()) {
+      check(qldpc_schedule_create(code, (int)lp.size() - 1, lp.data(), lr.data(), &sched));
+      ce.scheds.emplace(std::move(skey), sched);
+    } else {
+      sched = it->second;
+    }
+  }
+
+  const auto o = s.options();
+  at::Tensor ehat = ehat_bits ? at::empty({B, wn}, o.dtype(at::kLong)) : at::empty({B, n}, o.dtype(at::kByte));
+  at::Tensor iters = at::empty({B}, o.dtype(at::kInt));
+  at::Tensor post = at::empty({B, want_post ? n : 0}, o.dtype(at::kDouble));
+  at::Tensor flags = at::empty({B}, o.dtype(at::kInt));
+  if (B > 0) {
+    hipStream_t st = c10::hip::getCurrentHIPStream(dev).stream();
+    check(qldpc_decode_device_ex(code, sched, a, s.data_ptr(), fmt, B, p, (int)max_iter, beta, eps,
+                                 ehat.data_ptr(), ehat_bits ? QLDPC_FMT_BITS : QLDPC_FMT_BYTES,
+                                 iters.data_ptr<int32_t>(), want_post ? post.data_ptr<double>() : nullptr,
+                                 flags.data_ptr<int32_t>(), (void*)st));
+  }
+  return {ehat, iters, post, flags};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> decode_cpu(
+    const at::Tensor& syn, const at::Tensor&, const at::Tensor&, const at::Tensor&, double, int64_t,
+    c10::string_view, double, double, bool, bool) {
+  TORCH_CHECK_VALUE(false, "qldpc::decode runs on a HIP device: syndromes must be a device tensor (got ",
+                    syn.device(), ")");
+}
+
+}  // namespace
+
+TORCH_LIBRARY(qldpc, m) {
+  m.def("decode(Tensor syndromes, Tensor H, Tensor layer_ptr, Tensor layer_rows, float p, int max_iter, "
+        "str algo='MS', float beta=0.75, float eps=1e-09, bool want_post=False, bool ehat_bits=False) "
+        "-> (Tensor, Tensor, Tensor, Tensor)");
+}
+TORCH_LIBRARY_IMPL(qldpc, CUDA, m) { m.impl("decode", &decode_hip); }   // (HIP devices dispatch as CUDA)
+TORCH_LIBRARY_IMPL(qldpc, CPU, m) { m.impl("decode", &decode_cpu); }

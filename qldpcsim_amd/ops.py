@@ -1,16 +1,19 @@
-"""The batched decoder as a registered PyTorch operator (torch.library).
+"""The batched decoder as a registered PyTorch-ROCm C++ operator (torch.library).
 
     torch.ops.qldpc.decode(syndromes, H, layer_ptr, layer_rows, p, max_iter,
                            algo="MS", beta=0.75, eps=1e-9, want_post=False,
                            ehat_bits=False) -> (ehat, iters, post, flags)
 
 The same computation as decoders.decode_batch on a device tensor (the HIP
-kernels behind the C ABI, include/qldpc_decoder.h), exposed as a PyTorch-ROCm
-operator so that torch code (torch.compile graphs, custom pipelines) can call
-the decoder like any other op: it runs on torch's current stream of the
-syndromes' device and allocates its outputs through torch's caching
-allocator. Replaces, per batch, the reference's per-shot MS_decoder /
-BP_decoder calls (qLDPCsim/decoders.py:110-117, :189-195).
+kernels behind the C ABI, include/qldpc_decoder.h), registered from C++
+(qldpcsim_amd/csrc/torch_ops.cpp: TORCH_LIBRARY, HIP dispatch key) so that
+torch code (torch.compile graphs, custom pipelines) calls the decoder like any
+other op without Python in the call path: it runs on torch's current HIP
+stream of the syndromes' device, allocates its outputs through torch's
+caching allocator, and caches the Tanner graph and schedules per (device, H).
+The fake (meta) implementation below gives torch.compile the output shapes.
+Replaces, per batch, the reference's per-shot MS_decoder / BP_decoder calls
+(qLDPCsim/decoders.py:110-117, :189-195).
 
 Arguments: `syndromes` uint8 [B, m] (one byte per check) or int64
 [B, ceil(m/64)] (bit-packed words) on a HIP device; `H` the parity-check
@@ -20,38 +23,25 @@ ehat_bits), iters int32 [B], post float64 [B, n] (or [B, 0] unless
 want_post), flags int32 [B]. Errors as decode_batch: ValueError for shapes /
 options, RuntimeError for HIP failures; a CPU tensor raises (no CPU path).
 """
-import numpy as np
+import os
+
 import torch
 
-from . import decoders
+from . import _lib
 
-__all__ = ["decode"]
+__all__ = ["decode", "TORCH_OPS_PATH"]
 
-
-def _check_device(syndromes):
-    if syndromes.device.type != "cuda":
-        raise ValueError("qldpc::decode runs on a HIP device: syndromes must be a device tensor "
-                         f"(got {syndromes.device})")
-
-
-@torch.library.custom_op("qldpc::decode", mutates_args=())
-def decode(syndromes: torch.Tensor, H: torch.Tensor, layer_ptr: torch.Tensor, layer_rows: torch.Tensor,
-           p: float, max_iter: int, algo: str = "MS", beta: float = 0.75, eps: float = 1e-9,
-           want_post: bool = False, ehat_bits: bool = False
-           ) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
-    _check_device(syndromes)
-    Hn = H.detach().cpu().numpy()
-    lp = layer_ptr.detach().cpu().numpy().astype(np.int32)
-    lr = layer_rows.detach().cpu().numpy().astype(np.int32)
-    with torch.cuda.device(syndromes.device):
-        r = decoders.decode_batch(Hn, syndromes, p, max_iter, algo=algo, beta=beta, eps=eps,
-                                  want_post=want_post, layer_ptr=lp, layer_rows=lr, ehat_bits=ehat_bits)
-    post = r.post if r.post is not None else torch.empty((syndromes.shape[0], 0), dtype=torch.float64,
-                                                           device=syndromes.device)
-    return r.ehat, r.iters, post, r.flags
+# the C++ operator library (qldpcsim_amd/csrc/torch_ops.cpp, built in-tree by
+# __graft_entry__.build / make -C qldpcsim_amd/csrc torch); it links the
+# kernels' libqldpc_hip.so. No Python fallback: a missing build fails loudly.
+TORCH_OPS_PATH = os.path.join(os.path.dirname(_lib.LIB_PATH), "libqldpc_torch.so")
+if not os.path.exists(TORCH_OPS_PATH):
+    raise ImportError(f"{TORCH_OPS_PATH} is missing: build it with make -C qldpcsim_amd/csrc torch")
+torch.ops.load_library(TORCH_OPS_PATH)
+decode = torch.ops.qldpc.decode
 
 
-@decode.register_fake
+@torch.library.register_fake("qldpc::decode")
 def _(syndromes, H, layer_ptr, layer_rows, p, max_iter, algo="MS", beta=0.75, eps=1e-9,
       want_post=False, ehat_bits=False):
     B = syndromes.shape[0]

@@ -16,6 +16,10 @@ def _args(code="LP118_0", sched="L"):
 
 
 def test_op_is_registered_and_infers_shapes_on_meta():
+    # registered from C++ (torch_ops.cpp, TORCH_LIBRARY) by the in-tree library
+    assert ops.TORCH_OPS_PATH.endswith("qldpcsim_amd/_build/libqldpc_torch.so")
+    sch = str(torch.ops.qldpc.decode.default._schema)
+    assert sch.startswith("qldpc::decode(Tensor syndromes, Tensor H, Tensor layer_ptr, Tensor layer_rows")
     Hz, H, lp, lr = _args()
     m, n = Hz.shape
     syn = torch.empty((17, m), dtype=torch.uint8, device="meta")
