@@ -18,8 +18,8 @@
 // (and for CPU syndromes: there is no CPU path), IndexError for layer rows out
 // of range (decoders.py:156, :250), RuntimeError for HIP failures.
 #include <ATen/ATen.h>
-#include <c10/hip/HIPGuard.h>
-#include <c10/hip/HIPStream.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>   // ROCm torch: HIP devices carry DeviceType::CUDA
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/library.h>
 
 #include <map>
@@ -69,7 +69,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> decode_hip(
   else if (syn.scalar_type() == at::kLong && syn.size(1) == wm) fmt = QLDPC_FMT_BITS;
   else TORCH_CHECK_VALUE(false, "qldpc::decode: syndromes must be uint8 [B, ", m, "] or int64 words [B, ", wm, "]");
   const at::Tensor s = syn.contiguous();
-  const c10::hip::HIPGuard guard(s.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(s.device());
   const int dev = s.get_device();
 
   // graph and schedule, built once per (device, H) / layer partition
@@ -105,7 +105,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> decode_hip(
   at::Tensor post = at::empty({B, want_post ? n : 0}, o.dtype(at::kDouble));
   at::Tensor flags = at::empty({B}, o.dtype(at::kInt));
   if (B > 0) {
-    hipStream_t st = c10::hip::getCurrentHIPStream(dev).stream();
+    hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(dev).stream();
     check(qldpc_decode_device_ex(code, sched, a, s.data_ptr(), fmt, B, p, (int)max_iter, beta, eps,
                                  ehat.data_ptr(), ehat_bits ? QLDPC_FMT_BITS : QLDPC_FMT_BYTES,
                                  iters.data_ptr<int32_t>(), want_post ? post.data_ptr<double>() : nullptr,
