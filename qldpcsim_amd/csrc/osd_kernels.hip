@@ -282,6 +282,11 @@ __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
 //   D  every row applies its C to words w..: each update added a current
 //      pivot row = its block-start value + earlier pivot rows of the block.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t opaque_u32(uint32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 __device__ __forceinline__ uint32_t wave_or32(uint32_t x) {
   x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
   x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
@@ -356,6 +361,25 @@ __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL]
     }
     if (K < 32) pcl ^= 1u << K;
     else pch ^= 1u << (K - 32);
+#ifndef QLDPC_OSD_MASKED_XOR
+#define QLDPC_OSD_MASKED_XOR 1
+#endif
+#if QLDPC_OSD_MASKED_XOR
+    // Rows holding a 1 (above and below) take the pivot: x ^= p & mask with
+    // mask = 0 / ~0 from the column bit (one bit-field extract), the pivot
+    // row itself excluded — branch-free (v_bitop3), no exec-mask round trip
+    // from a VALU compare through SALU per slot. The low half is done in HI.
+    const uint32_t me = opaque_u32(lane == fl ? 0u : ~0u);
+#pragma unroll
+    for (int s = 0; s < SF; ++s) {
+      uint32_t mk = (uint32_t)__builtin_amdgcn_sbfe((int)(HI ? hi[s] : lo[s]), bit, 1);   // 0 / -1
+      mk &= (s == fs) ? me : ~0u;
+      if (!HI) lo[s] ^= plo & mk;
+      hi[s] ^= phi & mk;
+      cl[s] ^= pcl & mk;
+      ch[s] ^= pch & mk;
+    }
+#else
     const bool notme = lane != fl;
 #pragma unroll
     for (int s = 0; s < SF; ++s) {
@@ -366,6 +390,7 @@ __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL]
         ch[s] ^= pch;
       }
     }
+#endif
     const int wb = (HI ? 32 : 0) + bit;
     const int i = 64 * w + wb;
     pivm |= 1ull << wb;
