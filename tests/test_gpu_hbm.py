@@ -128,3 +128,32 @@ def test_forced_hbm_early_stopping_batch_equals_lds_kernels(monkeypatch):
     assert torch.equal(got.flags, ref.flags)
     assert torch.equal(got.post.view(torch.int64), ref.post.view(torch.int64))
     assert 1.0 < ref.iters.float().mean().item() < 20.0
+
+
+@pytest.mark.parametrize("B", [1, 63, 65, 1000])
+def test_forced_hbm_ragged_batches_and_edge_cases(B, monkeypatch):
+    """Batches that do not fill a 64-slot tile (1, 63, 65, 1000 half-shots),
+    all-zero syndromes (converged after the first iteration), max_iter = 1,
+    bit-packed I/O: the HBM kernel equals the LDS kernels on every output."""
+    import torch
+    from qldpcsim_amd import codes, decoders, schedule
+    Hx, Hz = codes.load_code("LP04_0")
+    rng = np.random.default_rng(B)
+    syn = rng.integers(0, 2, (B, Hz.shape[0]), dtype=np.uint8)
+    syn[::3] = 0
+    for sched in ("F", "L"):
+        lx, _ = schedule.select_layers(Hx, Hz, sched)
+        lp, lr = schedule.pack_layers(lx, Hz.shape[0])
+        for algo, it in (("MS", 1), ("MS", 30), ("BP", 1), ("BP", 12)):
+            s = decoders.pack_bits(torch.as_tensor(syn, device="cuda"))
+            monkeypatch.delenv("QLDPC_FORCE_HBM", raising=False)
+            ref = decoders.decode_batch(Hz, s, 0.03, it, algo=algo, want_post=True, layer_ptr=lp,
+                                        layer_rows=lr, ehat_bits=True)
+            monkeypatch.setenv("QLDPC_FORCE_HBM", "1")
+            got = decoders.decode_batch(Hz, s, 0.03, it, algo=algo, want_post=True, layer_ptr=lp,
+                                        layer_rows=lr, ehat_bits=True)
+            torch.cuda.synchronize()
+            assert torch.equal(got.iters, ref.iters) and torch.equal(got.ehat, ref.ehat), (sched, algo, it)
+            assert torch.equal(got.flags, ref.flags)
+            assert torch.equal(got.post.view(torch.int64), ref.post.view(torch.int64))
+            assert (got.iters[::3] == 1).all()                    # zero syndromes: converged at once
