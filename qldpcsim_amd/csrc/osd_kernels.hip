@@ -282,6 +282,14 @@ __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
 //   D  every row applies its C to words w..: each update added a current
 //      pivot row = its block-start value + earlier pivot rows of the block.
 // ---------------------------------------------------------------------------
+// v_writelane_b32 (value and lane select wave-uniform; the lane select in M0:
+// gfx9's constant bus takes one SGPR per instruction); the s_nop covers the
+// SALU-write -> lane-select read hazard the compiler cannot see in inline asm
+__device__ __forceinline__ int write_lane(int old, int value, int lane) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 4\n\tv_writelane_b32 %0, %1, m0" : "+v"(old) : "s"(value), "s"(lane) : "m0");
+  return old;
+}
+
 __device__ __forceinline__ uint32_t opaque_u32(uint32_t x) {
   asm volatile("" : "+v"(x));
   return x;
@@ -307,7 +315,7 @@ template <int SL, int SF, bool HI>
 __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL], uint32_t (&cl)[SL],
                                           uint32_t (&ch)[SL], uint64_t (&fm)[SL], uint32_t cols, int K,
                                           int w, int lane, int& rank, int& nJ, bool& done, uint64_t& pivm,
-                                          int rankH, int m, int* pk, int* Jl, unsigned char* inJ) {
+                                          int rankH, int m, int& pkv, int& ivv) {
   static_assert(SL <= 8, "the pivot-slot switch covers 8 slots");
   while (cols && !done) {
     // loop-carried scalars re-asserted wave-uniform: otherwise the compiler
@@ -394,13 +402,11 @@ __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL]
     const int wb = (HI ? 32 : 0) + bit;
     const int i = 64 * w + wb;
     pivm |= 1ull << wb;
-    if (lane == 0) {
-      pk[K] = (f << 6) | wb;
-      if (i != 0) {
-        Jl[nJ] = i;
-        inJ[i] = 1;
-      }
-    }
+    // pivot K's record (compact row << 6 | column bit) and column index go to
+    // lane K of two VGPRs (no exec-masked LDS store per pivot); the block's
+    // pk / Jl / inJ entries are written once after the engine loop
+    pkv = write_lane(pkv, (f << 6) | wb, K);
+    ivv = write_lane(ivv, i, K);
     if (i != 0) ++nJ;
     ++K;
     ++rank;
@@ -416,14 +422,14 @@ template <int SL, int SFMAX, bool HI>
 __device__ __forceinline__ int block_half_n(int SF, uint32_t (&lo)[SL], uint32_t (&hi)[SL], uint32_t (&cl)[SL],
                                             uint32_t (&ch)[SL], uint64_t (&fm)[SL], uint32_t cols, int K,
                                             int w, int lane, int& rank, int& nJ, bool& done, uint64_t& pivm,
-                                            int rankH, int m, int* pk, int* Jl, unsigned char* inJ) {
+                                            int rankH, int m, int& pkv, int& ivv) {
   if constexpr (SFMAX > 1) {
     if (SF <= SFMAX / 2)
       return block_half_n<SL, SFMAX / 2, HI>(SF, lo, hi, cl, ch, fm, cols, K, w, lane, rank, nJ, done, pivm,
-                                             rankH, m, pk, Jl, inJ);
+                                             rankH, m, pkv, ivv);
   }
-  return block_half<SL, SFMAX, HI>(lo, hi, cl, ch, fm, cols, K, w, lane, rank, nJ, done, pivm, rankH, m, pk,
-                                   Jl, inJ);
+  return block_half<SL, SFMAX, HI>(lo, hi, cl, ch, fm, cols, K, w, lane, rank, nJ, done, pivm, rankH, m, pkv,
+                                   ivv);
 }
 
 // SL = rows per wave-0 lane (m <= 64 SL), sized to the code so the state stays
@@ -587,10 +593,21 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
       const int SF = (F + 63) >> 6;
       uint64_t pivm = 0;
       // low half-word columns, then high (each loop's column order ascends)
+      const int nJ0 = nJ;
+      int pkv = 0, ivv = 0;
       int K = block_half_n<SL, SL, false>(SF, lo, hi, cl, ch, fm, (uint32_t)cols, 0, w, lane, rank, nJ, done,
-                                          pivm, a.rank, m, pk, Jl, inJ);
+                                          pivm, a.rank, m, pkv, ivv);
       K = block_half_n<SL, SL, true>(SF, lo, hi, cl, ch, fm, (uint32_t)(cols >> 32), K, w, lane, rank, nJ, done,
-                                     pivm, a.rank, m, pk, Jl, inJ);
+                                     pivm, a.rank, m, pkv, ivv);
+      // the block's J entries (column 0 is J's first entry from the start)
+      const int z = (K > 0 && __builtin_amdgcn_readlane(ivv, 0) == 0) ? 1 : 0;
+      if (lane < K) {
+        pk[lane] = pkv;
+        if (ivv != 0) {
+          Jl[nJ0 + lane - z] = ivv;
+          inJ[ivv] = 1;
+        }
+      }
 #pragma unroll
       for (int s = 0; s < SL; ++s) {
         const int cp = 64 * s + lane;
@@ -599,7 +616,7 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
       // (one wave: its LDS accesses complete in order, so these reads see
       // the writes above)
       if (lane < K) {
-        const int e = pk[lane];
+        const int e = pkv;
         const int row = crow[e >> 6];
         CT[e & 63] = Cm[row] ^ (1ull << lane);        // reduced pivot k = its own row + C
         pkof[row] = 64 * w + lane;
