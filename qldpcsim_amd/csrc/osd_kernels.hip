@@ -432,6 +432,51 @@ __device__ __forceinline__ int block_half_n(int SF, uint32_t (&lo)[SL], uint32_t
                                    ivv);
 }
 
+// XOR of the 64-bit table entries tab[k] over the set bits k of v, four
+// gathers in flight per trip
+__device__ __forceinline__ uint64_t osd_gather_xor4(const uint64_t* tab, uint64_t v) {
+  uint64_t acc = 0;
+  while (v) {
+    int k[4];
+    uint64_t mk[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      mk[j] = v ? ~0ull : 0ull;
+      k[j] = v ? (int)__builtin_ctzll(v) : 0;
+      v &= v - 1;
+    }
+    uint64_t c[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c[j] = tab[k[j]];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc ^= c[j] & mk[j];
+  }
+  return acc;
+}
+
+template <int NW, int W0>
+__device__ __forceinline__ void osd_apply_from(uint64_t (&R)[NW], uint64_t cm, const uint64_t* PW) {
+  while (cm) {
+    const int k = (int)__builtin_ctzll(cm);
+    cm &= cm - 1;
+    const uint64_t* src = PW + k * NW;
+    uint64_t v[NW - W0];
+#pragma unroll
+    for (int x = W0; x < NW; ++x) v[x - W0] = src[x];
+#pragma unroll
+    for (int x = W0; x < NW; ++x) R[x] ^= v[x - W0];
+  }
+}
+
+// R[x] ^= PW[k][x] for x >= w and every set bit k of cm (w wave-uniform)
+template <int NW, int W0 = 0>
+__device__ __forceinline__ void osd_apply_rows(uint64_t (&R)[NW], uint64_t cm, const uint64_t* PW, int w) {
+  if constexpr (W0 < NW) {
+    if (w == W0) osd_apply_from<NW, W0>(R, cm, PW);
+    else osd_apply_rows<NW, W0 + 1>(R, cm, PW, w);
+  }
+}
+
 // SL = rows per wave-0 lane (m <= 64 SL), sized to the code so the state stays
 // in VGPRs; RT = rows per thread (thread t holds rows t, t + blockDim, ..):
 // with 2, a 450-row shot takes 4 waves and a CU holds 4 shots (4 engines, one
@@ -667,25 +712,16 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
 #pragma unroll
         for (int x = 0; x < NW; ++x)
           if (x == w) v = R[h][x];
-        v &= pivm;
-        cm = 0;
-        while (v) {
-          cm ^= CT[__builtin_ctzll(v)];
-          v &= v - 1;
-        }
+        cm = osd_gather_xor4(CT, v & pivm);
       } else {
         cm = Cm[t + h * B];
       }
       // (per-lane gathers of the pivot rows: a uniform loop over all K with
-      // broadcast reads measured 2x slower, VALU-bound)
-      while (cm) {
-        const int k = (int)__builtin_ctzll(cm);
-        cm &= cm - 1;
-        const uint64_t* src = PW + k * NW;
-#pragma unroll
-        for (int x = 0; x < NW; ++x)
-          if (x >= w) R[h][x] ^= src[x];
-      }
+      // broadcast reads measured 2x slower, VALU-bound). The word range is a
+      // compile-time one per block (switch on w), so a pivot row's words are
+      // all read before any XOR — one LDS round trip per pivot row instead
+      // of one per word behind a uniform branch.
+      osd_apply_rows<NW>(R[h], cm, PW, w);
     }
     QLDPC_TICK(5);
   }
