@@ -121,6 +121,82 @@ __device__ __forceinline__ void put_ehat(const DecodeArgs& a, long long hs, int 
   }
 }
 
+// Read-only kernel inputs through the constant address space: with a
+// wave-uniform index the compiler issues scalar loads (through a generic
+// pointer it must assume the kernel's own stores alias them).
+template <typename T>
+__device__ __forceinline__ T ld_const(const T* p, long long i) {
+  return ((const __attribute__((address_space(4))) T*)p)[i];
+}
+
+// Syndrome bits of checks lane + 64 i (i < KC) of half-shot hs as bit i of
+// the result, every load issued before the first use: bit-packed rows are
+// KC wave-uniform words (scalar loads), byte rows KC per-lane loads at
+// clamped addresses (a guard around each load made the compiler wait after
+// each one).
+template <int KC>
+__device__ __forceinline__ uint32_t syn_lane_bits(const DecodeArgs& a, long long hs, int lane) {
+  const int m = a.m;
+  uint32_t r = 0;
+  if (a.syn_bits) {
+    const uint64_t* row = (const uint64_t*)a.syn + hs * a.wm;
+    uint64_t w[KC];
+#pragma unroll
+    for (int i = 0; i < KC; ++i) w[i] = ld_const(row, i < a.wm ? i : a.wm - 1);
+#pragma unroll
+    for (int i = 0; i < KC; ++i) {                  // (32-bit halves: no 64-bit VGPR shifts)
+      const uint32_t h = lane < 32 ? (uint32_t)w[i] : (uint32_t)(w[i] >> 32);
+      r |= (((h >> (lane & 31)) & 1u) & (uint32_t)(lane + 64 * i < m)) << i;
+    }
+  } else {
+    const uint8_t* row = a.syn + hs * (long long)m;
+    // (opaque lane: the clamped offsets are cheap to form here; hoisted out of
+    // the half-shot loop as invariants they cost VGPRs the decode loop needs)
+    uint32_t ln;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+    uint32_t b[KC];
+#pragma unroll
+    for (int i = 0; i < KC; ++i) b[i] = row[(int)ln + 64 * i < m ? (int)ln + 64 * i : m - 1];
+#pragma unroll
+    for (int i = 0; i < KC; ++i) r |= ((b[i] & 1u) & (uint32_t)(lane + 64 * i < m)) << i;
+  }
+  return r;
+}
+
+// ê (and posteriors) of one half-shot: original column jo = 64 k + lane takes
+// post_of(vinv[jo]) (the relabeled variable's posterior). Chunks of OC x 64
+// columns: the OC vinv loads, then the OC posterior reads, then the outputs —
+// one round trip per stage instead of one per column chunk (a guarded load
+// per chunk made the compiler wait after each one).
+template <int OC, typename Post>
+__device__ __forceinline__ void write_outputs_batched(const DecodeArgs& a, long long hs, int lane, Post post_of) {
+  const int n = a.n;
+  double* po = a.post ? a.post + hs * (long long)n : nullptr;
+  for (int k0 = 0; 64 * k0 < n; k0 += OC) {
+    int v[OC];
+#pragma unroll
+    for (int u = 0; u < OC; ++u) {
+      const int jo = 64 * (k0 + u) + lane;
+      v[u] = a.vinv[jo < n ? jo : n - 1];
+    }
+    double pv[OC];
+#pragma unroll
+    for (int u = 0; u < OC; ++u) pv[u] = post_of(v[u]);
+#pragma unroll
+    for (int u = 0; u < OC; ++u) {
+      const int jo = 64 * (k0 + u) + lane;
+      if (64 * (k0 + u) < n) {                       // (uniform; columns past n ballot 0)
+        if (a.eh_bits) {
+          put_ehat(a, hs, jo, jo < n && pv[u] < 0.0);
+        } else if (jo < n) {
+          put_ehat(a, hs, jo, pv[u] < 0.0);
+        }
+        if (po && jo < n) po[jo] = pv[u];
+      }
+    }
+  }
+}
+
 // Half-shot prologue / epilogue with every global load issued up front (a
 // loop of dependent load -> use steps paid one HBM latency per 64 elements).
 // The relabeling vinv is per code, so it is read once per kernel into
@@ -177,12 +253,19 @@ __device__ __forceinline__ void load_syndrome_bits(const DecodeArgs& a, long lon
   }
   const uint8_t* syn = a.syn + hs * (long long)m;
   if (m <= 64 * NC) {
+    // every load at a clamped address (a guarded load per chunk made the
+    // compiler wait after each one); the opaque lane keeps the offsets from
+    // being hoisted out of the half-shot loop into VGPRs
+    uint32_t ln;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
     uint32_t b[NC];
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
-      const int c = 64 * k + lane;
-      b[k] = (64 * k < m && c < m) ? (uint32_t)(syn[c] & 1) : 0u;
+      const int c = 64 * k + (int)ln;
+      b[k] = syn[c < m ? c : m - 1];
     }
+#pragma unroll
+    for (int k = 0; k < NC; ++k) b[k] = (64 * k + lane < m) ? (b[k] & 1u) : 0u;
 #pragma unroll
     for (int k = 0; k < NC; ++k)
       if (64 * k < m) store_bits64(synw, 64 * k, (int)b[k], lane);
@@ -1342,8 +1425,6 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
   const uint32_t post_b = lds_addr(colS), c2v_a = lds_addr(c2v_b);
   const int m = a.m, n = a.n;
   const float thr = a.hd_thresh;
-  VinvRegs<16> vr;                                             // n <= 1024 in registers
-  vr.load(a.vinv, n, lane);
 
   for (HalfShotQueue Q(a, waves, wid); Q.hs < a.batch; Q.advance()) {
     const long long hs = Q.hs;
@@ -1411,22 +1492,8 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
         }
       }
     }
-    {                                                          // ê, posteriors in original order
-      double* po = a.post ? a.post + hs * (long long)n : nullptr;
-      for (int k = 0; k < 16 && 64 * k < n; ++k) {
-        const int jo = 64 * k + lane;
-        if (jo < n) {
-          const double pv = L + (double)colS[n <= 1024 ? vr.get(k) : a.vinv[jo]];
-          put_ehat(a, hs, jo, pv < 0.0);
-          if (po) po[jo] = pv;
-        }
-      }
-      for (int jo = 1024 + lane; jo < n; jo += 64) {
-        const double pv = L + (double)colS[a.vinv[jo]];
-        put_ehat(a, hs, jo, pv < 0.0);
-        if (po) po[jo] = pv;
-      }
-    }
+    // ê, posteriors in original order (post = L + (f64)S, decoders.py:173-174)
+    write_outputs_batched<4>(a, hs, lane, [&](int v) { return L + (double)colS[v]; });
     const uint64_t b1 = ballot((fl & FLAG_MIN_ZERO) != 0);
     if (lane == 0) {
       a.iters[hs] = iters;

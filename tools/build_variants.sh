@@ -9,6 +9,7 @@ while [ $# -ge 2 ]; do
     tmp=$(mktemp -d)
     (cd "$ROOT" && git archive HEAD qldpcsim_amd/csrc include) | tar -x -C "$tmp"
     cp "$ROOT/qldpcsim_amd/csrc/Makefile" "$tmp/qldpcsim_amd/csrc/Makefile"
+    rm -f "$ROOT/qldpcsim_amd/_build/var_$name.so"   # archived sources carry old mtimes: make would skip
     make -s -C "$tmp/qldpcsim_amd/csrc" OUT_DIR="$ROOT/qldpcsim_amd/_build" LIB=var_$name.so 2>&1 | grep -i error || true
     rm -rf "$tmp"
   else
