@@ -163,20 +163,23 @@ __device__ __forceinline__ uint32_t syn_lane_bits(const DecodeArgs& a, long long
   return r;
 }
 
-// ê (and posteriors) of one half-shot: original column jo = 64 k + lane takes
-// post_of(vinv[jo]) (the relabeled variable's posterior). Chunks of OC x 64
-// columns: the OC vinv loads, then the OC posterior reads, then the outputs —
-// one round trip per stage instead of one per column chunk (a guarded load
-// per chunk made the compiler wait after each one).
-template <int OC, typename Post>
-__device__ __forceinline__ void write_outputs_batched(const DecodeArgs& a, long long hs, int lane, Post post_of) {
+// ê (and posteriors) of one half-shot: original column jo = ST k + t takes
+// post_of(vinv[jo]) (the relabeled variable's posterior); ST = 64 with t the
+// lane (one wave per half-shot) or the team size with t the thread index (a
+// wave's columns stay one aligned 64-column chunk). Chunks of OC trips: the
+// OC vinv loads, then the OC posterior reads, then the outputs — one round
+// trip per stage instead of one per trip (a guarded load per trip made the
+// compiler wait after each one).
+template <int OC, int ST, typename Post>
+__device__ __forceinline__ void write_outputs_strided(const DecodeArgs& a, long long hs, int t, Post post_of) {
   const int n = a.n;
+  const int cb = t & ~63;                            // this wave's chunk offset within a trip
   double* po = a.post ? a.post + hs * (long long)n : nullptr;
-  for (int k0 = 0; 64 * k0 < n; k0 += OC) {
+  for (int k0 = 0; ST * k0 < n; k0 += OC) {
     int v[OC];
 #pragma unroll
     for (int u = 0; u < OC; ++u) {
-      const int jo = 64 * (k0 + u) + lane;
+      const int jo = ST * (k0 + u) + t;
       v[u] = a.vinv[jo < n ? jo : n - 1];
     }
     double pv[OC];
@@ -184,8 +187,8 @@ __device__ __forceinline__ void write_outputs_batched(const DecodeArgs& a, long 
     for (int u = 0; u < OC; ++u) pv[u] = post_of(v[u]);
 #pragma unroll
     for (int u = 0; u < OC; ++u) {
-      const int jo = 64 * (k0 + u) + lane;
-      if (64 * (k0 + u) < n) {                       // (uniform; columns past n ballot 0)
+      const int jo = ST * (k0 + u) + t;
+      if (ST * (k0 + u) + cb < n) {                  // (wave-uniform; columns past n ballot 0)
         if (a.eh_bits) {
           put_ehat(a, hs, jo, jo < n && pv[u] < 0.0);
         } else if (jo < n) {
@@ -193,6 +196,30 @@ __device__ __forceinline__ void write_outputs_batched(const DecodeArgs& a, long 
         }
         if (po && jo < n) po[jo] = pv[u];
       }
+    }
+  }
+}
+template <int OC, typename Post>
+__device__ __forceinline__ void write_outputs_batched(const DecodeArgs& a, long long hs, int lane, Post post_of) {
+  write_outputs_strided<OC, 64>(a, hs, lane, post_of);
+}
+
+// syndrome bits of one half-shot into a team's word array: thread t covers
+// checks ST k + t, NT trips with their loads in flight together
+template <int NT, int ST>
+__device__ __forceinline__ void team_syndrome_bits(const DecodeArgs& a, long long hs, uint32_t* synw, int t) {
+  const int m = a.m, lane = t & 63, cb = t & ~63;
+  for (int k0 = 0; ST * k0 < m; k0 += NT) {
+    uint32_t b[NT];
+#pragma unroll
+    for (int u = 0; u < NT; ++u) {
+      const int c = ST * (k0 + u) + t;
+      b[u] = syn_bit(a, hs, c < m ? c : m - 1);
+    }
+#pragma unroll
+    for (int u = 0; u < NT; ++u) {
+      const int c0 = ST * (k0 + u) + cb;
+      if (c0 < m) store_bits64(synw, c0, (c0 + lane < m) ? (int)b[u] : 0, lane);
     }
   }
 }
@@ -1287,24 +1314,31 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
 // (S < hd_thresh is exactly L + (f64)S < 0). Each flipped hard decision
 // contributes its variable's filter word (stop test, ms_layered_kernel); the
 // lane-local XOR is returned.
-template <int K>
+// Variables per lane per pass: layers of more than 128 adjacent variables take
+// QLDPC_VN_H (4: LP118_2's 240 / 480 in one / two passes instead of two / four,
+// -6.5 % per launch), smaller ones 2 (a 4-wide pass over <= 128 variables
+// idles half its lanes: LP118_0 +4 %)
+#ifndef QLDPC_VN_H
+#define QLDPC_VN_H 4
+#endif
+template <int K, int H>
 __device__ __forceinline__ uint32_t vn_layer(const uint32_t* adj_info, const uint32_t* avar, float* colS,
                                              const float* c2v, int v0, int v1, int lane, float thr) {
   uint32_t acc = 0;
-  for (int qb = v0; qb < v1; qb += 128) {
-    uint32_t info[2];
-    bool in[2];
+  for (int qb = v0; qb < v1; qb += 64 * H) {
+    uint32_t info[H];
+    bool in[H];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < H; ++h) {
       const int q = qb + 64 * h + lane;
       in[h] = q < v1;
       info[h] = adj_info[in[h] ? q : v0];
     }
-    float old[2];
-    uint32_t av[2];
-    float x[2][K];
+    float old[H];
+    uint32_t av[H];
+    float x[H][K];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < H; ++h) {
       old[h] = colS[info[h] >> 21];                         // column sum before this layer
       av[h] = avar[info[h] >> 21];
       const float* c = c2v + (info[h] & 0xffffu);
@@ -1312,7 +1346,7 @@ __device__ __forceinline__ uint32_t vn_layer(const uint32_t* adj_info, const uin
       for (int t = 0; t < K; ++t) x[h][t] = c[t];          // c2v padded by 8 floats
     }
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < H; ++h) {
       const int d = (int)((info[h] >> 16) & 31u);
       float s = 0.0f;                                       // sequential, ascending check (:172)
 #pragma unroll
@@ -1446,13 +1480,16 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
     bool first = true;
     for (int it = 0; it < a.max_iter && !conv; ++it) {
       for (int l = 0; l < a.n_layers; ++l) {
-        const int q0 = lay_ptr[l], q1 = lay_ptr[l + 1];
+        const uint32_t dq = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uint32_t)lay_ptr[l] | ((uint32_t)lay_ptr[l + 1] << 16)));
+        const uint32_t dv = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uint32_t)adj_ptr[l] | ((uint32_t)adj_ptr[l + 1] << 16)));
+        const int dsel = __builtin_amdgcn_readfirstlane((int)adj_dmax[l]);
+        const int q0 = (int)(dq & 0xffffu), q1 = (int)(dq >> 16);
         if constexpr ((QLDPC_ABLATE_L & 1) != 0) {
         } else if constexpr (G != 0) {
           cn_layer<DC, G>(a, ltab, lrow, synw, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl);
         } else {
           // lanes per check chosen per layer by the host (bits 5-6 of adj_dmax)
-          switch (__builtin_amdgcn_readfirstlane((int)adj_dmax[l]) >> 5) {
+          switch (dsel >> 5) {
             case 0: cn_layer<DC, 1>(a, ltab, lrow, synw, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl); break;
             case 1: cn_layer<DC, 2>(a, ltab, lrow, synw, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl); break;
             case 2: cn_layer<DC, 4>(a, ltab, lrow, synw, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl); break;
@@ -1463,15 +1500,18 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
         wave_sync();
         // VN over the layer's adjacent variables (decoders.py:172-174: the
         // other columns are unchanged, so this equals the full recompute)
-        const int v0 = adj_ptr[l], v1 = adj_ptr[l + 1];
-        const int dmax = __builtin_amdgcn_readfirstlane((int)adj_dmax[l]) & 31;
+        const int v0 = (int)(dv & 0xffffu), v1 = (int)(dv >> 16);
+        const int dmax = dsel & 31;
         uint32_t acc = 0;
         switch ((QLDPC_ABLATE_L & 2) ? -1 : dmax) {
           case -1: break;
-          case 3: acc = vn_layer<3>(adj_info, avar, colS, c2v, v0, v1, lane, thr); break;
-          case 4: acc = vn_layer<4>(adj_info, avar, colS, c2v, v0, v1, lane, thr); break;
-          case 5: acc = vn_layer<5>(adj_info, avar, colS, c2v, v0, v1, lane, thr); break;
-          case 6: acc = vn_layer<6>(adj_info, avar, colS, c2v, v0, v1, lane, thr); break;
+#define QLDPC_VN_CASE(K)                                                                \
+  case K:                                                                               \
+    acc = v1 - v0 > 128 ? vn_layer<K, QLDPC_VN_H>(adj_info, avar, colS, c2v, v0, v1, lane, thr) \
+                        : vn_layer<K, 2>(adj_info, avar, colS, c2v, v0, v1, lane, thr);        \
+    break;
+          QLDPC_VN_CASE(3) QLDPC_VN_CASE(4) QLDPC_VN_CASE(5) QLDPC_VN_CASE(6)
+#undef QLDPC_VN_CASE
           default:
             for (int q = v0 + lane; q < v1; q += 64) {
               const uint32_t info = adj_info[q];
@@ -1647,10 +1687,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
     // initial parity) bit-words
     for (int j = tid; j < n; j += TS) post[j] = L;
     for (int p = tid; p < a.E; p += TS) c2v[p] = 0.0;
-    for (int c0 = 64 * wid; c0 < m; c0 += TS) {
-      const int c = c0 + lane;
-      store_bits64(synw, c0, c < m ? (int)syn_bit(a, hs, c) : 0, lane);
-    }
+    team_syndrome_bits<2, TS>(a, hs, synw, tid);
     __syncthreads();
 
     if constexpr (!LAYERED) {
@@ -1743,12 +1780,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
         }
       }
     }
-    double* po = a.post ? a.post + hs * (long long)n : nullptr;
-    for (int jo = tid; jo < n; jo += TS) {
-      const double pv = post[a.vinv[jo]];
-      put_ehat(a, hs, jo, pv < 0.0);                       // (:280)
-      if (po) po[jo] = pv;
-    }
+    write_outputs_strided<4, TS>(a, hs, tid, [&](int v) { return post[v]; });   // (:280)
     const bool nonfin = team_any((fl & FLAG_NONFINITE) != 0);
     if (tid == 0) {
       a.iters[hs] = iters;
@@ -1857,10 +1889,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
     rows_pf(0);
     for (int j = tid; j < n; j += TS) post[j] = L;      // (decoders.py:235-236)
     for (int p = tid; p < a.E; p += TS) c2v[p] = 0.0;
-    for (int c0 = 64 * wid; c0 < m; c0 += TS) {
-      const int c = c0 + lane;
-      store_bits64(synw, c0, c < m ? (int)syn_bit(a, hs, c) : 0, lane);
-    }
+    team_syndrome_bits<2, TS>(a, hs, synw, tid);
     __syncthreads();
     // stop test after every layer by the parity filters (bp_team_kernel)
     uint32_t bl = 0;
@@ -1933,12 +1962,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
         }
       }
     }
-    double* po = a.post ? a.post + hs * (long long)n : nullptr;
-    for (int jo = tid; jo < n; jo += TS) {
-      const double pv = post[a.vinv[jo]];
-      put_ehat(a, hs, jo, pv < 0.0);                       // (:280)
-      if (po) po[jo] = pv;
-    }
+    write_outputs_strided<4, TS>(a, hs, tid, [&](int v) { return post[v]; });   // (:280)
     const bool nonfin = team_any((fl & FLAG_NONFINITE) != 0);
     if (tid == 0) {
       a.iters[hs] = iters;
