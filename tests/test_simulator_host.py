@@ -31,6 +31,27 @@ def test_layer_counts_match_survey(name, nx, nz):
             assert H[l].sum(axis=0).max() <= 1
 
 
+def test_layers_equal_reference_layerize():
+    """schedule.select_layers equals the layers the reference's own layerize /
+    schedule selection (simulator.py:212-236, executed by
+    tests/golden/gen_golden_layers.py) builds for every bundled code, L and S,
+    cross-wiring included: layersX (from Hx) decodes Hz, layersZ decodes Hx."""
+    import json
+    import os
+    path = os.path.join(os.path.dirname(__file__), "golden", "schedules", "layers.npz")
+    with np.load(path, allow_pickle=False) as z:
+        keys = json.loads(bytes(z["index_json"]).decode())["keys"]
+        assert len(keys) == 4 * len(codes.available())
+        for key in keys:
+            name, sched, half = key.split("__")
+            Hx, Hz = codes.load_code(name)
+            lx, lz = schedule.select_layers(Hx, Hz, sched)
+            # (packed against the matrix the layers came from: a code whose Hx and Hz
+            # differ in rows would make pack_layers raise the reference's IndexError)
+            ptr, rows = schedule.pack_layers(lx if half == "X" else lz, (Hx if half == "X" else Hz).shape[0])
+            assert np.array_equal(ptr, z[key + "__ptr"]) and np.array_equal(rows, z[key + "__rows"]), key
+
+
 def test_serial_and_flooding_layers():
     Hx, Hz = codes.load_code("LP04_0")
     sx, sz = schedule.select_layers(Hx, Hz, "S")

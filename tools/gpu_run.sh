@@ -1,0 +1,100 @@
+# One parametrised GPU-box session (replaces the per-pass gpu_r0*.sh scripts).
+# usage: bash tools/gpu_run.sh TAG STEP [STEP ...]
+# steps (each under its own time limit; the session stops at the first failure):
+#   tests          full `pytest -m gpu`                       -> gpurun_out/TAG_pytest_gpu.log
+#   parity         decoder parity subset (parity, bits, osd)  -> gpurun_out/TAG_parity.log
+#   smoke          __graft_entry__.smoke()                    -> gpurun_out/TAG_smoke.log
+#   bench          bench.py --steps 20 --warmup 5 (headline)  -> gpurun_out/TAG_bench.log
+#   bench-cfg      bench.py on the configs[2]-[4] decoders    -> gpurun_out/TAG_bench_cfg.jsonl
+#   roof-decoders  counter profile (tools/gpu_profile_roofline.sh) of the configs[2]-[4] decoders
+#   roof-flood     counter profile of the headline kernel
+#   roof-hbm       counter profile of the HBM-resident kernel on the headline workload
+#   sim3 / sim4    tools/bench_sim.py p-sweep of configs[3] / configs[4]
+#   cfg3prof       per-kernel counters of one configs[3] p = 0.1 batch (tools/gpu_profile_program.sh)
+#   osd            tools/osd_bench.py on the configs[3] p = 0.1 OSD shots
+#   ab:LIBS:CFGS   interleaved A/B (tools/ab_libs.py) of qldpcsim_amd/_build/var_<name>.so builds;
+#                  LIBS = comma-separated names (main = the in-tree build), CFGS = cfg preset names
+#                  (flood, msl2p05, msl2p10, msl0, bpl2p10, bpl2p05, bpf0, hbm) joined by commas
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+TAG=$1; shift
+O=gpurun_out
+B=qldpcsim_amd/_build
+
+declare -A CFG=(
+  [flood]=""
+  [msl2p05]="--code LP118_2 --schedule L --p 0.05 --batch 262144"
+  [msl2p10]="--code LP118_2 --schedule L --p 0.1 --batch 131072"
+  [msl0]="--schedule L --batch 262144"
+  [bpl2p10]="--code LP118_2 --algo BP --schedule L --iters 100 --p 0.1 --batch 65536"
+  [bpl2p05]="--code LP118_2 --algo BP --schedule L --iters 100 --p 0.05 --batch 131072"
+  [bpf0]="--algo BP --iters 100 --batch 65536"
+  [hbm]="--path hbm --batch 262144 --hbm-leg 0"
+)
+
+fail() { echo "[$TAG] step $1 failed (rc=$2)"; [ -n "$3" ] && tail -8 "$3"; exit 1; }
+
+for step in "$@"; do
+  echo "[$TAG] $step"
+  case $step in
+    tests)
+      L=$O/${TAG}_pytest_gpu.log
+      timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread > $L 2>&1 || fail $step $? $L
+      tail -2 $L ;;
+    parity)
+      L=$O/${TAG}_parity.log
+      timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_bits.py tests/test_gpu_osd.py -m gpu -x -q \
+        --timeout 200 --timeout-method thread > $L 2>&1 || fail $step $? $L
+      tail -2 $L ;;
+    smoke)
+      L=$O/${TAG}_smoke.log
+      timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $L 2>&1 || fail $step $? $L
+      tail -2 $L ;;
+    bench)
+      L=$O/${TAG}_bench.log
+      timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $L 2>&1 || fail $step $? $L
+      tail -1 $L | cut -c1-300 ;;
+    bench-cfg)
+      L=$O/${TAG}_bench_cfg.jsonl
+      : > $L
+      for c in msl2p05 msl2p10 bpl2p10 bpf0; do
+        timeout -k 10 300 python bench.py --steps 5 --warmup 2 --cpu-seconds 0 --hbm-leg 0 ${CFG[$c]} >> $L 2> $O/${TAG}_bench_cfg.err || fail $step $? $O/${TAG}_bench_cfg.err
+      done
+      python3 -c "
+import json,sys
+for l in open('$L'):
+    d=json.loads(l); r=d['roofline']
+    print(d['config']['code'],d['config']['algo'],d['config']['schedule'],d['config']['p'],round(d['value']/1e6,3),'M', r['kernel'], r['bound'], r['frac'] and round(r['frac'],3))" ;;
+    roof-decoders)
+      bash tools/gpu_profile_roofline.sh $TAG msl2p05 "${CFG[msl2p05]}" msl2p10 "${CFG[msl2p10]}" \
+        bpl2p10 "${CFG[bpl2p10]}" bpf0 "${CFG[bpf0]}" || fail $step $? ;;
+    roof-flood)
+      bash tools/gpu_profile_roofline.sh ${TAG}f flood "" || fail $step $? ;;
+    roof-hbm)
+      bash tools/gpu_profile_roofline.sh ${TAG}h hbm "${CFG[hbm]}" || fail $step $? ;;
+    sim3|sim4)
+      L=$O/${TAG}_${step}.jsonl
+      [ $step = sim3 ] && W=LP118_2:MS || W=LP118_2:BP
+      timeout -k 10 700 python -u tools/bench_sim.py 1048576 $W > $L 2>&1 || fail $step $? $L
+      grep shots_per_s $L | cut -c1-160 ;;
+    cfg3prof)
+      bash tools/gpu_profile_program.sh ${TAG}_cfg3 tools/prof_sim.py LP118_2 MS L 0 50 0.1 131072 || fail $step $? ;;
+    osd)
+      L=$O/${TAG}_osd.log
+      timeout -k 10 300 python -u tools/osd_bench.py LP118_2 MS L 50 0.1 131072 0 5 > $L 2>&1 || fail $step $? $L
+      tail -4 $L ;;
+    ab:*)
+      IFS=: read -r _ libs cfgs <<< "$step"
+      A=()
+      for l in ${libs//,/ }; do [ $l = main ] && A+=($B/libqldpc_hip.so) || A+=($B/var_$l.so); done
+      C=()
+      for c in ${cfgs//,/ }; do C+=(--cfg "${CFG[$c]}"); done
+      L=$O/${TAG}_ab_${libs//,/_}.json
+      timeout -k 10 900 python -u tools/ab_libs.py --rounds 3 "${C[@]}" "${A[@]}" > $L 2>&1 || fail $step $? $L
+      cat $L ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "[$TAG] done"
