@@ -85,15 +85,33 @@ __device__ __forceinline__ double qldpc_div_dev(double a, double b) {
   return qldpc_fma_dev(rem, r, q);
 }
 #define QLDPC_DIV(a, b) qldpc_div_dev((a), (b))
+/* the same v_fma_f64 with a wave-uniform addend taken from an SGPR pair (a
+   library constant): a "v" operand made the compiler copy every constant
+   into VGPRs with a v_mov_b64 per use */
+__device__ __forceinline__ double qldpc_fma_dev_s(double a, double b, double c) {
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+  return r;
+}
+#define QLDPC_FMA_K(a, b, c) qldpc_fma_dev_s((a), (b), (c))
+/* ... and with a wave-uniform multiplier b */
+__device__ __forceinline__ double qldpc_fma_dev_sb(double a, double b, double c) {
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c));
+  return r;
+}
+#define QLDPC_FMA_KB(a, b, c) qldpc_fma_dev_sb((a), (b), (c))
 #else
 #define QLDPC_FMA(a, b, c) __builtin_fma((a), (b), (c))
+#define QLDPC_FMA_K(a, b, c) __builtin_fma((a), (b), (c))
+#define QLDPC_FMA_KB(a, b, c) __builtin_fma((a), (b), (c))
 #define QLDPC_DIV(a, b) ((a) / (b))
 #endif
 
 /* the table image: NumPy's tanh intervals (rows b, c0 .. c16 as [9][16][2]
    row pairs), SVML atanh's log(1 + i/16) [16][2] (hi, lo) and its
    reciprocal step buckets */
-typedef struct {
+typedef struct __attribute__((aligned(16))) {   /* 16-byte pair reads on the device */
   double tanh_c[16 * 18];
   double atanh_hl[16 * 2];
   uint32_t atanh_rcp[64];
@@ -109,7 +127,21 @@ QLDPC_HD double qldpc_tanh_t(double x, const double* tc) {
   h = h < 0 ? 0 : h;
   h = h > 0x780000 ? 0x780000 : h;
   const double* c = tc + 2 * (h >> 19);               /* interval 0 .. 15; row k at c[32 (k/2) + k%2] */
+#if defined(__HIP_DEVICE_COMPILE__)
+  /* the nine coefficient pairs as 16-byte LDS reads (ds_read_b128: 4 LDS
+     cycles, conflict-free across intervals), all issued before the Horner
+     chain; as double loads the compiler emitted ds_read2_b64 (8 cycles,
+     2-way conflicts between intervals i and i + 8) with a wait before each
+     step. Same coefficients, same operations. */
+  typedef double qldpc_d2 __attribute__((ext_vector_type(2)));
+  const qldpc_d2* c2 = (const qldpc_d2*)c;            /* pair j (rows 2j, 2j+1) at c2[16 j] */
+  qldpc_d2 q[9];
+#pragma unroll
+  for (int j = 0; j < 9; ++j) q[j] = c2[16 * j];
+#define QLDPC_TC(k) q[(k) / 2][(k) & 1]
+#else
 #define QLDPC_TC(k) c[32 * ((k) / 2) + ((k) & 1)]
+#endif
   const double y = qldpc_bits2d(u & 0x7fffffffffffffffull) - QLDPC_TC(0);
   double r = QLDPC_TC(17);
   r = QLDPC_FMA(r, y, QLDPC_TC(16));
@@ -167,29 +199,37 @@ QLDPC_HD double qldpc_atanh_t(double x, const double* hl, const uint32_t* rb) {
   const double dp = QLDPC_FMA(Yp_lo, Rp, QLDPC_FMA(Rp, Yp, -1.0));   /* Rp (1 + ax) - 1 */
   const double dm = QLDPC_FMA(-Ym_nlo, Rm, QLDPC_FMA(Ym, Rm, -1.0)); /* Rm (1 - ax) - 1 */
   const double ediff = gm - gp;
-  double Pp = QLDPC_FMA(QLDPC_ATANH_C0, dp, QLDPC_ATANH_C1);
-  double Pm = QLDPC_FMA(QLDPC_ATANH_C0, dm, QLDPC_ATANH_C1);
-  const double K = QLDPC_FMA(QLDPC_ATANH_LN2HI, ediff, hl[2 * im] - hl[2 * ip]);
-  Pp = QLDPC_FMA(dp, Pp, QLDPC_ATANH_C2);
-  Pm = QLDPC_FMA(dm, Pm, QLDPC_ATANH_C2);
-  Pp = QLDPC_FMA(dp, Pp, QLDPC_ATANH_C3);
-  Pm = QLDPC_FMA(dm, Pm, QLDPC_ATANH_C3);
-  const double Klo = QLDPC_FMA(QLDPC_ATANH_LN2LO, ediff, hl[2 * im + 1] - hl[2 * ip + 1]);
+#if defined(__HIP_DEVICE_COMPILE__)
+  /* (hi, lo) of log(1 + i/16) as one 16-byte LDS read per index */
+  typedef double qldpc_d2 __attribute__((ext_vector_type(2)));
+  const qldpc_d2 hm = ((const qldpc_d2*)hl)[im], hp = ((const qldpc_d2*)hl)[ip];
+  const double hdiff = hm[0] - hp[0], ldiff = hm[1] - hp[1];
+#else
+  const double hdiff = hl[2 * im] - hl[2 * ip], ldiff = hl[2 * im + 1] - hl[2 * ip + 1];
+#endif
+  double Pp = QLDPC_FMA_K(dp, QLDPC_ATANH_C0, QLDPC_ATANH_C1);   /* C0 dp + C1 (fma commutes a, b) */
+  double Pm = QLDPC_FMA_K(dm, QLDPC_ATANH_C0, QLDPC_ATANH_C1);
+  const double K = QLDPC_FMA_KB(ediff, QLDPC_ATANH_LN2HI, hdiff);
+  Pp = QLDPC_FMA_K(dp, Pp, QLDPC_ATANH_C2);
+  Pm = QLDPC_FMA_K(dm, Pm, QLDPC_ATANH_C2);
+  Pp = QLDPC_FMA_K(dp, Pp, QLDPC_ATANH_C3);
+  Pm = QLDPC_FMA_K(dm, Pm, QLDPC_ATANH_C3);
+  const double Klo = QLDPC_FMA_KB(ediff, QLDPC_ATANH_LN2LO, ldiff);
   const double dp2 = dp * dp;
-  Pp = QLDPC_FMA(dp, Pp, QLDPC_ATANH_C4);
-  Pm = QLDPC_FMA(dm, Pm, QLDPC_ATANH_C4);
+  Pp = QLDPC_FMA_K(dp, Pp, QLDPC_ATANH_C4);
+  Pm = QLDPC_FMA_K(dm, Pm, QLDPC_ATANH_C4);
   const double S1 = dp + K;
-  Pp = QLDPC_FMA(dp, Pp, QLDPC_ATANH_C5);
-  Pm = QLDPC_FMA(dm, Pm, QLDPC_ATANH_C5);
+  Pp = QLDPC_FMA_K(dp, Pp, QLDPC_ATANH_C5);
+  Pm = QLDPC_FMA_K(dm, Pm, QLDPC_ATANH_C5);
   const double dm2 = dm * dm;
-  Pp = QLDPC_FMA(dp, Pp, QLDPC_ATANH_C6);
-  Pm = QLDPC_FMA(dm, Pm, QLDPC_ATANH_C6);
+  Pp = QLDPC_FMA_K(dp, Pp, QLDPC_ATANH_C6);
+  Pm = QLDPC_FMA_K(dm, Pm, QLDPC_ATANH_C6);
   const double t4 = K - S1;
   const double S2 = S1 - dm;
-  Pp = QLDPC_FMA(dp, Pp, QLDPC_ATANH_C7);
-  Pm = QLDPC_FMA(dm, Pm, QLDPC_ATANH_C7);
-  Pp = QLDPC_FMA(dp, Pp, QLDPC_ATANH_C8);
-  Pm = QLDPC_FMA(dm, Pm, QLDPC_ATANH_C8);
+  Pp = QLDPC_FMA_K(dp, Pp, QLDPC_ATANH_C7);
+  Pm = QLDPC_FMA_K(dm, Pm, QLDPC_ATANH_C7);
+  Pp = QLDPC_FMA_K(dp, Pp, QLDPC_ATANH_C8);
+  Pm = QLDPC_FMA_K(dm, Pm, QLDPC_ATANH_C8);
   const double e1 = dp + t4;                           /* rounding error of S1 */
   const double t5 = S2 - S1;
   const double A = QLDPC_FMA(dp2, Pp, Klo);
