@@ -75,7 +75,7 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="bounded CPU-baseline sample per leg (0 disables)")
     ap.add_argument("--path", default="auto", choices=["auto", "hbm"],
-                    help="hbm: decode through the HBM-resident kernel (QLDPC_FORCE_HBM=1) in the timed region")
+                    help="hbm: decode through the HBM-resident kernel (library option force_hbm) in the timed region")
     ap.add_argument("--hbm-leg", type=int, default=1,
                     help="N=1: also time the same workload through the HBM-resident kernel (hbm_streaming field)")
     ap.add_argument("--worklog", default=None,
@@ -87,27 +87,11 @@ def parse(argv=None):
 # host facts
 # ---------------------------------------------------------------------------
 def host_cores():
-    """CPU cores this process may use: the affinity mask, capped by a cgroup
-    CPU quota and by OMP_NUM_THREADS (the GPU box sets it to the box's CPU
-    share). Returns (cores, how)."""
-    try:
-        n = len(os.sched_getaffinity(0))
-        how = ["sched_getaffinity"]
-    except AttributeError:
-        n, how = os.cpu_count() or 1, ["os.cpu_count"]
-    try:
-        with open("/sys/fs/cgroup/cpu.max") as f:
-            q, per = f.read().split()[:2]
-        if q != "max":
-            c = max(1, int(float(q) / float(per)))
-            if c < n:
-                n, how = c, how + ["cgroup cpu.max"]
-    except (OSError, ValueError):
-        pass
-    omp = os.environ.get("OMP_NUM_THREADS", "")
-    if omp.isdigit() and 0 < int(omp) < n:
-        n, how = int(omp), how + ["OMP_NUM_THREADS"]
-    return n, " capped by ".join(how)
+    """CPU cores this process may use (qldpcsim_amd/hostcores.py): the
+    affinity mask, capped by a cgroup CPU quota and by OMP_NUM_THREADS (the
+    GPU box sets it to the box's CPU share). Returns (cores, how)."""
+    from qldpcsim_amd import hostcores
+    return hostcores.process_cores()
 
 
 def device_code_sha(path):
@@ -365,9 +349,9 @@ def run_rank(args, rank, world, local):
         else:
             dist.init_process_group(backend)
 
-    if args.path == "hbm":
-        os.environ["QLDPC_FORCE_HBM"] = "1"
     from qldpcsim_amd import _lib, codes, decoders, schedule
+    if args.path == "hbm":
+        _lib.set_option("force_hbm", 1)
     from qldpcsim_amd.simulator import DeviceChannel
     Hx, Hz = codes.load_code(args.code)
     m, n = Hz.shape
@@ -503,13 +487,12 @@ def run_rank(args, rank, world, local):
 
 def hbm_streaming_leg(halves, outs, prior, args, B, bits, algo_launch, dev, steps=2):
     """The same workload through hbm_tile_kernel (message state in HBM, every
-    message a coalesced 256-byte tile row; QLDPC_FORCE_HBM=1): SURVEY.md
+    message a coalesced 256-byte tile row; option force_hbm): SURVEY.md
     §8(d)'s HBM roofline is the bound of that design. Reported beside the
     headline (which is the LDS-resident kernel's), untimed by the headline."""
     import torch
     from qldpcsim_amd import _lib, decoders
-    os.environ["QLDPC_FORCE_HBM"] = "1"
-    try:
+    with _lib.options(force_hbm=1):
         name = _lib.kernel_name(halves[0][0], halves[0][2], halves[0][3], args.algo, dev.index)
 
         def step():
@@ -527,8 +510,6 @@ def hbm_streaming_leg(halves, outs, prior, args, B, bits, algo_launch, dev, step
         el = time.perf_counter() - t0
         kern_ms, launches = _lib.timing_read()
         _lib.timing_enable(False)
-    finally:
-        os.environ.pop("QLDPC_FORCE_HBM", None)
     t_launch = kern_ms / 1e3 / launches
     gbs = algo_launch / t_launch / 1e9
     measured = None
@@ -540,7 +521,7 @@ def hbm_streaming_leg(halves, outs, prior, args, B, bits, algo_launch, dev, step
             "kernel_ms_per_launch": t_launch * 1e3, "algorithmic_gbs": gbs, "peak_gbs": HBM_PEAK_GBS,
             "frac": gbs / HBM_PEAK_GBS,
             "note": "the same workload and iteration counts through the HBM-resident decoder "
-                    "(QLDPC_FORCE_HBM=1); GB/s under SURVEY.md 8d's algorithmic model (the kernel moves "
+                    "(option force_hbm); GB/s under SURVEY.md 8d's algorithmic model (the kernel moves "
                     "about 1.27x those bytes: post and c2v rows both read per edge); the headline value is "
                     "the LDS-resident kernel's"}
 
@@ -586,15 +567,22 @@ def roofline(names, t_launch, hs_launch, it_launch, algo_launch, launches):
         valu = pu["valu_insts"] * it_launch / t_launch / 1e9             # G wave-instructions / s
         valu_peak = SIMDS * CLOCK_GHZ / VALU_CYCLES
         valu_unit = "G VALU wave-instructions/s (4 cycles each)"
-    lds = pu["lds_cycles"] * it_launch / t_launch / 1e9              # G LDS-array cycles / s (chip)
+    # LDS: array cycles plus the stores' extra transfer cycles when the
+    # profile has the store counts (path cycles, MI355X_MICROARCH.md §LDS:
+    # ds_write_b32 4 / b64 6 cycles against 2 / 4 array cycles)
+    lds_cyc = pu.get("lds_path_cycles", pu["lds_cycles"])
+    lds = lds_cyc * it_launch / t_launch / 1e9                       # G LDS cycles / s (chip)
+    lds_array = pu["lds_cycles"] * it_launch / t_launch / 1e9
     lds_peak = CUS * CLOCK_GHZ
     traffic = prof["per_half_shot"]["hbm_bytes"] * hs_launch
     hbm_gbs = traffic / t_launch / 1e9                                # measured (PMC) HBM bytes
     units = {"valu": {"achieved": valu, "peak": valu_peak, "unit": valu_unit,
                       "frac": valu / valu_peak,
                       "frac_lo": None if valu_lo is None else valu_lo / valu_peak},
-             "lds": {"achieved": lds, "peak": lds_peak, "unit": "G LDS-array cycles/s (all CUs)",
-                     "frac": lds / lds_peak},
+             "lds": {"achieved": lds, "peak": lds_peak,
+                     "unit": ("G LDS cycles/s (all CUs): array + store transfer" if "lds_path_cycles" in pu
+                              else "G LDS-array cycles/s (all CUs)"),
+                     "frac": lds / lds_peak, "frac_array": lds_array / lds_peak},
              "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s (measured HBM bytes)",
                      "frac": hbm_gbs / HBM_PEAK_GBS}}
     bound = max(units, key=lambda k: units[k]["frac"])
@@ -604,7 +592,8 @@ def roofline(names, t_launch, hs_launch, it_launch, algo_launch, launches):
     r["formula"] = ("valu frac = valu_cycles/half-shot-iter x iterations/launch / (1024 SIMDs x 2.4 GHz x "
                     "launch time), valu_cycles = 2 x SQ_INSTS_VALU + 2 x (ADD+MUL+FMA_F64) + 14 x TRANS_F64 + "
                     "6 x TRANS_F32 (per-class SQ_INSTS_VALU_* counters) + 2 x the unclassified rest "
-                    "(float64 min/max/compare have no class counter; frac_lo leaves it out); lds frac = lds_cycles/half-shot-iter x "
+                    "(float64 min/max/compare have no class counter; frac_lo leaves it out); lds frac = (SQ_LDS_IDX_ACTIVE + 2 x "
+                    "SQ_INSTS_LDS_STORE: array + store transfer cycles)/half-shot-iter x "
                     "iterations/launch / (256 CUs x 2.4 GHz x launch time); hbm frac = PMC HBM bytes/half-shot x "
                     "half-shots/launch / launch time / 8000 GB/s; bound = the largest; per-unit counts from the "
                     "profile (SQ_INSTS_VALU, SQ_LDS_IDX_ACTIVE; traffic = 2 x FETCH_SIZE + WRITE_SIZE), "

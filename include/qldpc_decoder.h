@@ -22,8 +22,11 @@
  *    Device entry points are asynchronous on that stream and do no
  *    allocation, copy or synchronisation (hipGraph-capturable).
  *  - Results are bit-exact with the reference for MS (hard decisions,
- *    iteration counts, float64 posteriors) and within
- *    1e-5 relative on BP posteriors (device tanh/atanh; App. A.2).
+ *    iteration counts, float64 posteriors) and for BP,
+ *    whose tanh / arctanh / log restate the NumPy 2.2.6 / SVML functions the
+ *    reference runs on the capture host (include/qldpc_libm.h); against other
+ *    NumPy builds the north star's 1e-5 relative contract on BP posteriors
+ *    (App. A.2) is what holds.
  */
 #ifndef QLDPC_DECODER_H
 #define QLDPC_DECODER_H
@@ -83,6 +86,11 @@ int qldpc_code_shape(const qldpc_code *code, int *m, int *n, int *n_edges);
 int qldpc_schedule_create(const qldpc_code *code, int n_layers, const int32_t *h_layer_ptr,
                           const int32_t *h_layer_rows, qldpc_schedule **out);
 int qldpc_schedule_destroy(qldpc_schedule *sched);
+/* Frees the schedule's HBM-resident-kernel workspace (grown on demand, up to
+ * half of the free device memory; kept between launches otherwise), after
+ * the last launch that used it has finished. The next HBM decode allocates
+ * it again. */
+int qldpc_schedule_release_workspace(qldpc_schedule *sched);
 
 /* Batched decode, device pointers, asynchronous on `stream`.
  * Replaces `batch` calls of MS_decoder / BP_decoder (without the OSD
@@ -251,6 +259,27 @@ int qldpc_count_outcomes(const qldpc_code *hx, const qldpc_code *hz, int64_t bat
 int qldpc_timing_enable(int on);
 int qldpc_timing_reset(void);
 int qldpc_timing_read(double *total_ms, int64_t *launches);
+
+/* Library options: which kernel family decodes, for tests (every variant is
+ * checked against the oracle), A/B experiments and diagnostics. The defaults
+ * are the measured best and what the product runs; the library never reads
+ * the environment. A change applies from the next launch on, for every
+ * schedule. Names (default):
+ *   "force_hbm" (0)           every code through the HBM-resident kernel
+ *   "flood_generic" (0)       flooding MS through decode_kernel, not ms_flood_kernel
+ *   "layered_generic" (0)     layered MS through decode_kernel, not ms_layered_kernel
+ *   "ms_lanes_per_check" (0)  layered MS: one lanes-per-check width for every layer (0: per layer)
+ *   "bp_wave" (0)             BP through the one-wave decode_kernel, not the team kernels
+ *   "bp_lg" (1)               layered BP: the global-table team kernel (0: tables in LDS)
+ *   "bp_team_w" (0)           BP team width in waves (0: automatic)
+ *   "static_sched" (0)        static half-shot striding instead of the work queue
+ *   "waves_per_wg" (0), "wg_per_cu" (0)   occupancy overrides of the wave kernels
+ *   "osd_column" (0)          GPU OSD through the exact-REF column kernel only
+ *   "osd_tickets" (1)         GPU OSD engine wave placed by per-CU SIMD tickets
+ *   "osd_prof" (0)            print per-phase OSD cycles (builds with QLDPC_OSD_TIMING)
+ * Unknown name: QLDPC_EINVAL. */
+int qldpc_set_option(const char *name, int64_t value);
+int qldpc_get_option(const char *name, int64_t *value);
 
 #ifdef __cplusplus
 }

@@ -4,6 +4,7 @@ The product path has no CPU fallback: if the HIP library is missing this
 module raises on import, and every decode entry point fails loudly when no
 HIP device is visible.
 """
+import contextlib
 import ctypes
 import os
 import threading
@@ -22,13 +23,14 @@ FMT_BYTES, FMT_BITS = 0, 1          # syndrome / estimate formats (QLDPC_FMT_*)
 EXPORTS = (
     "qldpc_last_error", "qldpc_version", "qldpc_device_count",
     "qldpc_code_create", "qldpc_code_destroy", "qldpc_code_shape",
-    "qldpc_schedule_create", "qldpc_schedule_destroy",
+    "qldpc_schedule_create", "qldpc_schedule_destroy", "qldpc_schedule_release_workspace",
     "qldpc_decode_device", "qldpc_decode_device_ex", "qldpc_decode_host", "qldpc_decode_kernel_name",
     "qldpc_osd_decode", "qldpc_osd_decode_batch", "qldpc_osd_device", "qldpc_osd_order_device",
     "qldpc_osd_device_ordered", "qldpc_osd_device_ordered_ex", "qldpc_cpython_setdiff_first",
     "qldpc_channel_thresholds", "qldpc_channel_sample", "qldpc_channel_sample_ex", "qldpc_count_outcomes",
     "qldpc_count_outcomes_ex",
     "qldpc_timing_enable", "qldpc_timing_reset", "qldpc_timing_read",
+    "qldpc_set_option", "qldpc_get_option",
 )
 
 
@@ -62,6 +64,7 @@ def _load():
         "qldpc_code_shape": ([P, P, P, P], I),
         "qldpc_schedule_create": ([P, I, P, P, PP], I),
         "qldpc_schedule_destroy": ([P], I),
+        "qldpc_schedule_release_workspace": ([P], I),
         "qldpc_decode_device": ([P, P, I, P, I64, D, I, D, D, P, P, P, P, P], I),
         "qldpc_decode_device_ex": ([P, P, I, P, I, I64, D, I, D, D, P, I, P, P, P, P], I),
         "qldpc_decode_host": ([P, P, I, P, I64, D, I, D, D, P, P, P, P], I),
@@ -81,9 +84,16 @@ def _load():
         "qldpc_timing_enable": ([I], I),
         "qldpc_timing_reset": ([], I),
         "qldpc_timing_read": ([P, P], I),
+        "qldpc_set_option": ([ctypes.c_char_p, I64], I),
+        "qldpc_get_option": ([ctypes.c_char_p, P], I),
     }
     for name, (args, res) in sig.items():
-        fn = getattr(L, name)
+        try:
+            fn = getattr(L, name)
+        except AttributeError:
+            if "QLDPC_LIB" in os.environ:       # an older A/B build (tools/build_variants.sh HEAD)
+                continue
+            raise
         fn.argtypes = args
         fn.restype = res
     return L
@@ -203,6 +213,17 @@ except ImportError:                                     # the normalising path a
 _code_fast = {}
 
 
+def release_hbm_workspaces():
+    """qldpc_schedule_release_workspace on every cached schedule."""
+    with _code_lock:
+        codes_ = list({id(c): c for c in list(_code_cache.values()) + list(_code_fast.values())}.values())
+    for c in codes_:
+        with c._lock:
+            scheds = list(c._sched.values())
+        for s in scheds:
+            check(lib.qldpc_schedule_release_workspace(s.handle))
+
+
 def kernel_name(H, layer_ptr, layer_rows, algo, device_index=None):
     """Name of the decode kernel a launch for (H, schedule, algo) uses."""
     code = code_for(H, device_index)
@@ -225,3 +246,37 @@ def timing_read():
     n = ctypes.c_int64()
     check(lib.qldpc_timing_read(ctypes.byref(ms), ctypes.byref(n)))
     return ms.value, n.value
+
+
+# ---------------------------------------------------------------------------
+# library options (qldpc_set_option): which kernel family decodes. The
+# library never reads the environment; QLDPC_OPTIONS="name=value,..." is
+# applied once here, at import (A/B tools start one process per setting).
+# ---------------------------------------------------------------------------
+def set_option(name, value):
+    check(lib.qldpc_set_option(name.encode(), int(value)))
+
+
+def get_option(name):
+    v = ctypes.c_int64()
+    check(lib.qldpc_get_option(name.encode(), ctypes.byref(v)))
+    return v.value
+
+
+@contextlib.contextmanager
+def options(**kw):
+    """Set library options for the duration of a block, e.g.
+    `with options(force_hbm=1): ...`; the previous values come back after."""
+    old = {k: get_option(k) for k in kw}
+    try:
+        for k, v in kw.items():
+            set_option(k, v)
+        yield
+    finally:
+        for k, v in old.items():
+            set_option(k, v)
+
+
+for _kv in filter(None, os.environ.get("QLDPC_OPTIONS", "").split(",")):
+    _k, _, _v = _kv.partition("=")
+    set_option(_k.strip(), int(_v or 1))

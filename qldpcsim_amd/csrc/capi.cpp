@@ -64,6 +64,56 @@ extern "C" int qldpc_device_count(void) {
 }
 
 // ---------------------------------------------------------------------------
+// options (include/qldpc_decoder.h): read at launch, never from the
+// environment; `gen` changes with every set so cached launch configurations
+// are rebuilt
+// ---------------------------------------------------------------------------
+namespace {
+struct Options {
+  std::atomic<int64_t> force_hbm{0}, flood_generic{0}, layered_generic{0}, ms_lanes_per_check{0}, bp_wave{0},
+      bp_lg{1}, bp_team_w{0}, static_sched{0}, waves_per_wg{0}, wg_per_cu{0}, osd_column{0}, osd_tickets{1},
+      osd_prof{0};
+  std::atomic<uint32_t> gen{1};
+};
+Options g_opt;
+
+std::atomic<int64_t>* option_slot(const char* name) {
+  if (!name) return nullptr;
+  static const struct {
+    const char* name;
+    std::atomic<int64_t> Options::*slot;
+  } table[] = {{"force_hbm", &Options::force_hbm},     {"flood_generic", &Options::flood_generic},
+               {"layered_generic", &Options::layered_generic},
+               {"ms_lanes_per_check", &Options::ms_lanes_per_check},
+               {"bp_wave", &Options::bp_wave},         {"bp_lg", &Options::bp_lg},
+               {"bp_team_w", &Options::bp_team_w},     {"static_sched", &Options::static_sched},
+               {"waves_per_wg", &Options::waves_per_wg}, {"wg_per_cu", &Options::wg_per_cu},
+               {"osd_column", &Options::osd_column},   {"osd_tickets", &Options::osd_tickets},
+               {"osd_prof", &Options::osd_prof}};
+  for (const auto& e : table)
+    if (strcmp(e.name, name) == 0) return &(g_opt.*(e.slot));
+  return nullptr;
+}
+
+int64_t opt(std::atomic<int64_t> Options::*slot) { return (g_opt.*slot).load(std::memory_order_relaxed); }
+}  // namespace
+
+extern "C" int qldpc_set_option(const char* name, int64_t value) {
+  std::atomic<int64_t>* o = option_slot(name);
+  if (!o) return fail(QLDPC_EINVAL, "unknown option %s", name ? name : "(null)");
+  o->store(value);
+  g_opt.gen.fetch_add(1);
+  return QLDPC_OK;
+}
+
+extern "C" int qldpc_get_option(const char* name, int64_t* value) {
+  std::atomic<int64_t>* o = option_slot(name);
+  if (!o || !value) return fail(QLDPC_EINVAL, "unknown option %s", name ? name : "(null)");
+  *value = o->load();
+  return QLDPC_OK;
+}
+
+// ---------------------------------------------------------------------------
 // code (Tanner graph)
 // ---------------------------------------------------------------------------
 struct qldpc_code {
@@ -269,6 +319,8 @@ struct LaunchCfg {
   bool lblob = false;  // uses the layer-ordered blob (ms_layered_kernel)
   bool gtab = false;     // ms_flood_kernel: global tables, LDS = wave state only
   bool tlg = false;      // bp_team_lg_kernel: every table global, LDS image = layer pointers
+  bool hbm = false;      // the LDS kernels cannot hold this schedule: hbm_tile_kernel (cached)
+  uint32_t gen = 0;      // g_opt.gen the configuration was built under
   int team = 0;          // bp_team_kernel: waves per half-shot (one workgroup), 0 = wave kernels
   const char* name = "";  // kernel name as rocprofv3 reports it
   bool ok = false;
@@ -310,6 +362,7 @@ struct qldpc_schedule {
   void* hbm_ws = nullptr;
   size_t hbm_ws_bytes = 0;
   hipEvent_t hbm_ev = nullptr;
+  int hbm_tiles_cap[2] = {0, 0};  // per algo: CUs x resident tiles per CU (queried once)
   // half-shot work-queue counters (ring: concurrent launches on different
   // streams take different slots; each is zeroed on the launch stream)
   static constexpr int kQueueSlots = 64;
@@ -607,6 +660,18 @@ extern "C" int qldpc_schedule_destroy(qldpc_schedule* s) {
   return QLDPC_OK;
 }
 
+extern "C" int qldpc_schedule_release_workspace(qldpc_schedule* s) {
+  if (!s) return fail(QLDPC_EINVAL, "schedule is null");
+  std::lock_guard<std::mutex> lk(s->mu);
+  if (s->hbm_ws) {
+    if (s->hbm_ev) HIP_TRY(hipEventSynchronize(s->hbm_ev));   // the last launch that used it is done
+    HIP_TRY(hipFree(s->hbm_ws));
+    s->hbm_ws = nullptr;
+    s->hbm_ws_bytes = 0;
+  }
+  return QLDPC_OK;
+}
+
 // per-wave state slice: post f64[n] | c2v (f32|f64)[E] | syn words | parity words
 static void wave_layout(const qldpc_code* c, bool layered, int algo, int* bytes, int* off_c2v,
                         int* off_synw, int* off_parw, bool colsum_f32 = false) {
@@ -641,29 +706,31 @@ static void team_layout(const qldpc_code* c, int w, int* bytes, int* off_c2v, in
 static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   std::lock_guard<std::mutex> lk(s->mu);
   LaunchCfg& cfg = s->cfg[algo];
-  if (cfg.ok) {
+  const uint32_t gen = g_opt.gen.load();
+  if (cfg.ok && cfg.gen == gen) {
     *out = &cfg;
     return QLDPC_OK;
   }
+  cfg = LaunchCfg{};
   const qldpc_code* c = s->code;
   const int dc = fast_table_ok(c) ? c->uniform_deg : 0;
   cfg.kernel = nullptr;
   int max_waves = QLDPC_MAX_THREADS / 64;
   bool gtab = false;
-  if (algo == QLDPC_ALGO_MS && !s->layered && dc > 0 && !s->fblob.empty() && !getenv("QLDPC_NO_REGTAB")) {
+  if (algo == QLDPC_ALGO_MS && !s->layered && dc > 0 && !s->fblob.empty() && !opt(&Options::flood_generic)) {
     cfg.kernel = qldpc::select_ms_flood_kernel(dc, (c->m + 63) / 64, &cfg.name);
     gtab = cfg.kernel != nullptr;
     if (gtab) max_waves = qldpc::ms_flood_max_waves((c->m + 63) / 64);
   }
   bool use_lblob = false;
   if (!cfg.kernel && algo == QLDPC_ALGO_MS && s->layered && dc > 0 && !s->lblob.empty() &&
-      !getenv("QLDPC_NO_LAYERED_FAST")) {
+      !opt(&Options::layered_generic)) {
     // lanes per check: 8 for one- or two-row layers (serial schedules), else
     // one (interleaved A/B, DESIGN.md §3.2: wider groups lost on 7-60-row layers)
     // lanes per check: one template width when every layer wants the same,
     // else chosen per layer (the runtime switch costs ~5 % where it is not needed)
     int g = s->layer_g > 0 ? s->layer_g : 0;
-    if (const char* ev = getenv("QLDPC_MS_LANES_PER_CHECK")) g = atoi(ev);
+    if (const int64_t og = opt(&Options::ms_lanes_per_check)) g = (int)og;
     // (several half-shots per wave, ms_layered_grp_kernel, measured 2x slower
     // in round 2: at a fixed LDS budget it halves the waves per CU; removed)
     cfg.kernel = qldpc::select_ms_layered_kernel(dc, g, &cfg.name);
@@ -672,7 +739,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   cfg.lblob = use_lblob;
   cfg.gtab = gtab;
   int team = 0;
-  if (!cfg.kernel && algo == QLDPC_ALGO_BP && dc > 0 && !getenv("QLDPC_BP_WAVE")) {
+  if (!cfg.kernel && algo == QLDPC_ALGO_BP && dc > 0 && !opt(&Options::bp_wave)) {
     // 4 waves per half-shot; 8 when a team's LDS footprint leaves at most 3
     // teams per CU (LP118_2: 67 KB), so a CU still runs >= 16 waves
     int tb = 0, o1, o2, o3, o4;
@@ -684,11 +751,10 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
     // tables, 3 with the row table alone global; the kernel is barrier /
     // latency-bound and BP-L p = 0.1 ran 175 -> 132 -> 108 ms per launch.
     // Schedules without the global image (n > 2048, a column degree > 31) run
-    // the all-LDS team kernel; QLDPC_BP_LG=0 forces it (tests).
-    bool tlg = s->layered && !s->lgblob.empty();
-    if (const char* ev = getenv("QLDPC_BP_LG")) tlg = tlg && atoi(ev) != 0;
+    // the all-LDS team kernel; option bp_lg = 0 forces it (tests).
+    const bool tlg = s->layered && !s->lgblob.empty() && opt(&Options::bp_lg) != 0;
     if (tlg) team = 4;
-    if (const char* ev = getenv("QLDPC_BP_TEAM_W")) team = atoi(ev);
+    if (const int64_t ow = opt(&Options::bp_team_w)) team = (int)ow;
     if (tlg) {
       cfg.kernel = qldpc::select_bp_team_lg_kernel(dc, team, &cfg.name);
       cfg.tlg = cfg.kernel != nullptr;
@@ -734,9 +800,9 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
       cfg.lds = lds;
     }
   }
-  // Tuning overrides (experiments only): QLDPC_WAVES_PER_WG, QLDPC_WG_PER_CU.
-  if (const char* ev = team ? nullptr : getenv("QLDPC_WAVES_PER_WG")) {
-    const int w = atoi(ev);
+  // Tuning overrides (experiments only): options waves_per_wg, wg_per_cu.
+  if (const int64_t ow = team ? 0 : opt(&Options::waves_per_wg)) {
+    const int w = (int)ow;
     const int lds = blob + w * cfg.wave_bytes + libm;
     int nb = 0;
     if (w >= 1 && w <= max_waves && lds <= max_lds &&
@@ -747,14 +813,16 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
       best_waves = nb * w;
     }
   }
-  if (const char* ev = getenv("QLDPC_WG_PER_CU")) {
-    const int k = atoi(ev);
+  if (const int64_t ok = opt(&Options::wg_per_cu)) {
+    const int k = (int)ok;
     if (k >= 1 && k < cfg.blocks_per_cu) cfg.blocks_per_cu = k;
   }
-  if (best_waves == 0)
-    return fail(QLDPC_EUNSUP, "graph needs %d B of LDS per wave plus %d B of tables: exceeds %d B",
-                cfg.wave_bytes, blob, max_lds);
+  // no LDS kernel holds the graph's per-half-shot state and tables: the
+  // HBM-resident kernel decodes it (choose_path); decided once per
+  // configuration, not per launch
+  cfg.hbm = best_waves == 0;
   cfg.ok = true;
+  cfg.gen = gen;
   *out = &cfg;
   return QLDPC_OK;
 }
@@ -809,19 +877,15 @@ extern "C" int qldpc_timing_read(double* total_ms, int64_t* launches) {
 // ---------------------------------------------------------------------------
 // Which kernel family decodes (schedule, algo): the LDS-resident kernels when
 // their tables and per-half-shot state fit, else the HBM-resident kernel
-// (hbm_kernels.hip). QLDPC_FORCE_HBM=1 takes the HBM kernel for any code
+// (hbm_kernels.hip). Option force_hbm takes the HBM kernel for any code
 // (tests: the two families agree bit for bit).
 static int choose_path(qldpc_schedule* s, int algo, LaunchCfg** cfg, bool* hbm) {
   const qldpc_code* c = s->code;
-  const char* ev = getenv("QLDPC_FORCE_HBM");
-  *hbm = !s->lds_ok || (ev && atoi(ev) != 0) || (algo == QLDPC_ALGO_MS && c->max_row_deg > 32) ||
+  *hbm = !s->lds_ok || opt(&Options::force_hbm) != 0 || (algo == QLDPC_ALGO_MS && c->max_row_deg > 32) ||
          (algo == QLDPC_ALGO_BP && c->max_col_deg > 128);
   if (*hbm) return QLDPC_OK;
   const int rc = launch_config(s, algo, cfg);
-  if (rc == QLDPC_EUNSUP) {                      // LDS image / state does not fit a CU
-    *hbm = true;
-    return QLDPC_OK;
-  }
+  if (rc == QLDPC_OK && (*cfg)->hbm) *hbm = true;   // LDS image / state does not fit a CU
   return rc;
 }
 
@@ -836,20 +900,31 @@ static int decode_hbm(const qldpc_code* code, qldpc_schedule* s, int algo, const
                       int ehat_format, int32_t* d_iters, double* d_post, int32_t* d_flags, hipStream_t st) {
   const char* name = nullptr;
   const void* kern = qldpc::select_hbm_kernel(algo, code->max_row_deg, &name);
-  if (!kern) return fail(QLDPC_EUNSUP, "row degree %d exceeds the HBM kernel's 64", code->max_row_deg);
-  int dev = 0, cus = 0;
-  HIP_TRY(hipGetDevice(&dev));
-  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  if (!kern) return fail(QLDPC_EINVAL, "Unrecognized decoder type.");
   const size_t w = algo == QLDPC_ALGO_MS ? 4 : 8;   // message / posterior row element (MS: f32 S)
   const size_t per_tile = ((size_t)code->E * w + (size_t)code->n * w + (size_t)code->m) * 64;
   std::lock_guard<std::mutex> lk(s->mu);
-  size_t free_b = 0, total_b = 0;
-  HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-  const size_t budget = std::min<size_t>(free_b / 2 + s->hbm_ws_bytes, (size_t)64 << 30);
-  int per_cu = 0;
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * qldpc::kHbmWaves, 0));
-  int64_t tiles = std::min<int64_t>((batch + 63) / 64, (int64_t)cus * std::max(per_cu, 1));
-  tiles = std::min<int64_t>(tiles, (int64_t)(budget / per_tile));
+  if (s->hbm_tiles_cap[algo] == 0) {               // resident tiles: queried once per schedule
+    int dev = 0, cus = 0, per_cu = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * qldpc::kHbmWaves, 0));
+    s->hbm_tiles_cap[algo] = cus * std::max(per_cu, 1);
+  }
+  int64_t tiles = std::min<int64_t>((batch + 63) / 64, (int64_t)s->hbm_tiles_cap[algo]);
+  // the workspace those tiles need; grown (never shrunk: qldpc_schedule_release_workspace
+  // frees it) within half of the free device memory, at most 64 GiB
+  auto need_of = [&](int64_t t) {
+    const size_t op = ((size_t)t * code->E * w * 64 + 255) & ~(size_t)255;
+    const size_t os = (op + (size_t)t * code->n * w * 64 + 255) & ~(size_t)255;
+    return os + (size_t)t * code->m * 64 + 256;
+  };
+  if (need_of(tiles) > s->hbm_ws_bytes) {
+    size_t free_b = 0, total_b = 0;
+    HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+    const size_t budget = std::min<size_t>(free_b / 2 + s->hbm_ws_bytes, (size_t)64 << 30);
+    tiles = std::min<int64_t>(tiles, (int64_t)(budget / per_tile));
+  }
   if (tiles < 1) return fail(QLDPC_EUNSUP, "HBM decode needs %zu B per 64-slot tile: device memory too small", per_tile);
   const size_t off_post = ((size_t)tiles * code->E * w * 64 + 255) & ~(size_t)255;
   const size_t off_syn = (off_post + (size_t)tiles * code->n * w * 64 + 255) & ~(size_t)255;
@@ -1041,7 +1116,7 @@ extern "C" int qldpc_decode_device_ex(const qldpc_code* code, const qldpc_schedu
   }
 
   a.queue = nullptr;
-  if (!getenv("QLDPC_STATIC_SCHED")) {
+  if (!opt(&Options::static_sched)) {
     a.queue = sched->d_queue + (sched->qnext.fetch_add(1) % qldpc_schedule::kQueueSlots);
   }
   int cus = 0;
@@ -1084,8 +1159,7 @@ extern "C" int qldpc_decode_kernel_name(const qldpc_code* code, const qldpc_sche
   int rc = choose_path(sched, algo, &cfg, &hbm);
   if (rc) return rc;
   const char* hname = nullptr;
-  if (hbm && !qldpc::select_hbm_kernel(algo, code->max_row_deg, &hname))
-    return fail(QLDPC_EUNSUP, "row degree %d exceeds the HBM kernel's 64", code->max_row_deg);
+  if (hbm) (void)qldpc::select_hbm_kernel(algo, code->max_row_deg, &hname);
   snprintf(buf, (size_t)len, "%s", hbm ? hname : cfg->name);
   return QLDPC_OK;
 }
@@ -1489,7 +1563,6 @@ extern "C" int qldpc_osd_device_ordered_ex(const qldpc_code* code, int64_t count
 static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t* d_syn, const int32_t* d_perm,
                            const int32_t* d_tiepos, const double* d_post, int order, uint8_t* d_ehat,
                            int32_t* d_status, void* stream) {
-  if (code) code_osd_prep(code);
   if (!code) return fail(QLDPC_EINVAL, "code is null");
   if (count < 0) return fail(QLDPC_EINVAL, "negative count");
   if (count == 0) return QLDPC_OK;
@@ -1505,9 +1578,8 @@ static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t*
   // H[:, perm] has no pivot (an all-zero column of H: column kernel for the
   // whole code) or the syndrome lies outside H's column space (the block
   // kernel marks those shots, a second column-kernel pass redoes them).
-  // QLDPC_OSD_KERNEL=column: the column kernel alone (A/B reference).
-  const char* kenv = getenv("QLDPC_OSD_KERNEL");
-  const bool column = (kenv && strcmp(kenv, "column") == 0) || code->zero_col;
+  // option osd_column: the column kernel alone (A/B reference, tests).
+  const bool column = opt(&Options::osd_column) != 0 || code->zero_col;
   int rt = 1;                                        // block kernel: rows per thread
   const void* kblk = column ? nullptr : qldpc::select_osd_block_kernel(nw, m, &rt);
   const int block = std::max(64, (m + 63) / 64 * 64);
@@ -1524,6 +1596,9 @@ static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t*
   HIP_TRY(hipFuncSetAttribute(kcol, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds));
   if (kblk && lds_blk > max_lds) kblk = nullptr;
   if (kblk) HIP_TRY(hipFuncSetAttribute(kblk, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds));
+  // rank(H) and the column bit-vectors: built on first use, after every
+  // cheap refusal above (a large HBM-path code is refused without them)
+  code_osd_prep(code);
   qldpc::OsdArgs a{};
   a.row_ptr = code->d_row_ptr;
   a.col_idx = code->d_col_idx;
@@ -1544,7 +1619,7 @@ static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t*
     a.spill_cap = g_spill.cap;
   }
   static unsigned long long* d_prof = nullptr;       // diagnostic builds (QLDPC_OSD_TIMING)
-  if (getenv("QLDPC_OSD_PROF") && !d_prof) {
+  if (opt(&Options::osd_prof) && !d_prof) {
     HIP_TRY(hipMalloc(&d_prof, 16 * sizeof(unsigned long long)));
     HIP_TRY(hipMemset(d_prof, 0, 16 * sizeof(unsigned long long)));
   }
@@ -1555,11 +1630,12 @@ static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t*
     static std::mutex mu;
     static uint32_t* tickets[64] = {};
     std::lock_guard<std::mutex> lk(mu);
-    if (dev >= 0 && dev < 64 && !tickets[dev] && !getenv("QLDPC_OSD_NO_TICKETS")) {
+    const bool use_tickets = opt(&Options::osd_tickets) != 0;
+    if (dev >= 0 && dev < 64 && !tickets[dev] && use_tickets) {
       HIP_TRY(hipMalloc(&tickets[dev], sizeof(uint32_t) * qldpc::kOsdCuSlots));
       HIP_TRY(hipMemset(tickets[dev], 0, sizeof(uint32_t) * qldpc::kOsdCuSlots));
     }
-    a.cu_tickets = (dev >= 0 && dev < 64 && !getenv("QLDPC_OSD_NO_TICKETS")) ? tickets[dev] : nullptr;
+    a.cu_tickets = (dev >= 0 && dev < 64 && use_tickets) ? tickets[dev] : nullptr;
   }
   int64_t done = 0;
   while (done < count) {  // grid.x limit

@@ -33,14 +33,8 @@
 #include <stdint.h>
 
 #include "decoder_kernels.h"
+#include "tuning.h"
 #include "../../include/qldpc_libm.h"
-
-#ifndef QLDPC_ABLATE
-#define QLDPC_ABLATE 0  // timing-only builds: 1 = skip VN, 2 = skip CN (flooding)
-#endif
-#ifndef QLDPC_ABLATE_L
-#define QLDPC_ABLATE_L 0  // timing-only builds of ms_layered_kernel: bit 0 skips CN, bit 1 VN, bit 2 the filter
-#endif
 
 namespace qldpc {
 
@@ -1035,14 +1029,14 @@ __device__ __forceinline__ void vn_run(const DecodeArgs& a, double* post, const 
   const float* c = c2v + p0 + lane * K;
   double* po = post + start + lane;
   int o0 = 0;
-#ifndef QLDPC_VN_NOPAIR
-  for (; o0 + 128 <= count; o0 += 128) {
-    const float s0 = vn_sum<K>(c + o0 * K);
-    const float s1 = vn_sum<K>(c + (o0 + 64) * K);
-    po[o0] = a.L + (double)s0;
-    po[o0 + 64] = a.L + (double)s1;
+  if constexpr (QLDPC_VN_PAIR != 0) {
+    for (; o0 + 128 <= count; o0 += 128) {
+      const float s0 = vn_sum<K>(c + o0 * K);
+      const float s1 = vn_sum<K>(c + (o0 + 64) * K);
+      po[o0] = a.L + (double)s0;
+      po[o0 + 64] = a.L + (double)s1;
+    }
   }
-#endif
   for (; o0 + 64 <= count; o0 += 64) po[o0] = a.L + (double)vn_sum<K>(c + o0 * K);
   if (o0 + lane < count) po[o0] = a.L + (double)vn_sum<K>(c + o0 * K);
 }
@@ -1059,9 +1053,6 @@ __device__ __forceinline__ void vn_run_any(const DecodeArgs& a, double* post, co
 
 template <int KC>
 constexpr int ms_flood_max_threads() { return KC >= 8 ? 512 : 256; }
-#ifndef QLDPC_FLOOD_WPE
-#define QLDPC_FLOOD_WPE 3  // waves per SIMD the register budget targets (KC <= 4)
-#endif
 template <int KC>
 constexpr int ms_flood_wpe() { return KC >= 8 ? 2 : QLDPC_FLOOD_WPE; }
 
@@ -1318,9 +1309,6 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
 // QLDPC_VN_H (4: LP118_2's 240 / 480 in one / two passes instead of two / four,
 // -6.5 % per launch), smaller ones 2 (a 4-wide pass over <= 128 variables
 // idles half its lanes: LP118_0 +4 %)
-#ifndef QLDPC_VN_H
-#define QLDPC_VN_H 4
-#endif
 template <int K, int H>
 __device__ __forceinline__ uint32_t vn_layer(const uint32_t* adj_info, const uint32_t* avar, float* colS,
                                              const float* c2v, int v0, int v1, int lane, float thr) {

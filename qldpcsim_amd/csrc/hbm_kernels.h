@@ -4,15 +4,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "tuning.h"
+
 namespace qldpc {
 
 // One workgroup of kHbmWaves waves = one tile of 64 half-shot slots (lane l =
 // slot l); every lane of a wave walks the same check / variable at the same
 // time, so graph reads are wave-uniform (scalar loads) and message reads are
 // coalesced: tile g's element i of slot l at [g][i][64].
-#ifndef QLDPC_HBM_WAVES
-#define QLDPC_HBM_WAVES 4
-#endif
 constexpr int kHbmWaves = QLDPC_HBM_WAVES;   // (kernel names in hbm_kernels.hip spell out 4)
 struct HbmArgs {
   // graph (relabeled variables, int32, global)

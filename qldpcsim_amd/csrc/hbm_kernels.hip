@@ -95,9 +95,6 @@ __global__ void __launch_bounds__(64 * W) hbm_tile_kernel(HbmArgs a, const int32
                                                         const int32_t* __restrict__ fl_pos, int lazy) {
   using Msg = typename std::conditional<ALGO == ALGO_MS, float, double>::type;
   using Post = Msg;                                 // MS: float32 column sum S; BP: float64 posterior
-#ifndef QLDPC_HBM_UC
-#define QLDPC_HBM_UC 1
-#endif
   constexpr int UC = QLDPC_HBM_UC;                   // checks per load step (1: 16 waves per CU; 2: 12, 4: 8 — slower, r03o)
   constexpr int UV = 4, KV = 8;                   // variables per load batch, messages loaded up front
   __shared__ uint32_t xb[3][W * 64];              // per-wave partials: [0] filters / flags, [1] stop test, [2] B
@@ -129,9 +126,58 @@ __global__ void __launch_bounds__(64 * W) hbm_tile_kernel(HbmArgs a, const int32
     else return POST(v);
   };
 
+  // Check node of a row of more than DCMAX edges (rows of any degree decode,
+  // as the reference's load_matrix takes any H): the same arithmetic in two
+  // passes over the edges in CSR (ascending variable) order — pass 1 forms
+  // min1 / min2 and the sign parity (MS) or np.prod's sequential fold (BP),
+  // pass 2 re-forms each edge's v2c (its own c2v is still the old one: each
+  // edge is read before it is written) and writes the new message.
+  int fl = 0;
+  auto cn_wide = [&](int e0, int d, uint32_t sbit, bool first, int l, bool lzf) {
+    auto v2c = [&](int k) -> double {                 // post - c2v of edge k (:155-156, :247-248)
+      const int e = e0 + k, var = tb(a.row_var, e), pos = tb(a.row_pos, e);
+      if (ALGO == ALGO_MS && first && l == 0) return (double)a.L32;   // msg_v2c = float32(L) (:148-149)
+      const bool okv = !lzf || !first || tb(fl_var, var) < l;
+      const bool okc = !lzf || !first || tb(fl_pos, pos) < l;
+      return (okv ? rd_post(var) : L) - (double)(okc ? C2V(pos) : (Msg)0);
+    };
+    if constexpr (ALGO == ALGO_MS) {
+      uint32_t par = sbit;
+      double min1 = __builtin_inf(), min2 = __builtin_inf();
+      for (int k = 0; k < d; ++k) {
+        const double v = v2c(k);
+        par ^= (uint32_t)(v < 0.0);                   // np.sign, 0 -> +1 (:157-158)
+        const double x = __builtin_fabs(v);
+        min2 = __builtin_fmin(min2, __builtin_fmax(min1, x));   // min of the rest (:162-164)
+        min1 = __builtin_fmin(min1, x);
+      }
+      const double m1 = __builtin_isinf(min1) ? 0.0 : min1, m2 = __builtin_isinf(min2) ? 0.0 : min2;
+      if (m1 == 0.0) fl |= FLAG_MIN_ZERO;
+      const float c1 = (float)(a.beta * m1), c2 = (float)(a.beta * m2);   // (:167-168)
+      for (int k = 0; k < d; ++k) {
+        const double v = v2c(k);
+        const float mag = (__builtin_fabs(v) == min1) ? c2 : c1;
+        C2V(tb(a.row_pos, e0 + k)) = ((uint32_t)(v < 0.0) ^ par) ? -mag : mag;
+      }
+    } else {
+      double prod = 1.0;
+      for (int k = 0; k < d; ++k) prod *= qldpc_tanh_t(v2c(k) / 2.0, lt->tanh_c);   // np.prod (:254)
+      for (int k = 0; k < d; ++k) {
+        const double th = qldpc_tanh_t(v2c(k) / 2.0, lt->tanh_c);
+        if (th == 0.0) fl |= FLAG_NONFINITE;
+        double th2 = prod / th;                                        // (:256)
+        th2 = (__builtin_fabs(th2) >= 1.0 - a.eps) ? th2 - __builtin_copysign(a.eps, th2) : th2;
+        double val = 2.0 * qldpc_atanh_t(th2, lt->atanh_hl, lt->atanh_rcp);   // (:259)
+        if (sbit) val = -val;                                          // (:260-261)
+        if (!__builtin_isfinite(val)) fl |= FLAG_NONFINITE;
+        C2V(tb(a.row_pos, e0 + k)) = val;
+      }
+    }
+  };
+
   long long shot = -1;
   bool need = true;          // take a half-shot at the next iteration boundary (same on every wave)
-  int it = 0, fl = 0, lstop = 0;
+  int it = 0, lstop = 0;
   uint32_t F = 0, B = 0;
 
   for (;;) {
@@ -249,6 +295,10 @@ __global__ void __launch_bounds__(64 * W) hbm_tile_kernel(HbmArgs a, const int32
           for (int u = 0; u < UC; ++u) {
             const int d = dg[u];
             if (!act || d == 0) continue;
+            if (d > DCMAX) {                            // (uniform) a row wider than the kernel's
+              cn_wide(e0[u], d, sb[u], first, l, lzf);  // registers: two passes over its edges
+              continue;
+            }
             if constexpr (ALGO == ALGO_MS) {
               double av[DCMAX];
               uint64_t negm = 0;
@@ -453,10 +503,13 @@ __global__ void __launch_bounds__(64 * W) hbm_tile_kernel(HbmArgs a, const int32
     if (name) *name = "hbm_tile_kernel<" #A ", " #D ", 4>";                                    \
     return (const void*)&hbm_tile_kernel<ALG, D, kHbmWaves>;                                   \
   }
+// (rows past 64 edges take the 64-wide instance's two-pass cn_wide)
 const void* select_hbm_kernel(int algo, int dcmax, const char** name) {
-  QLDPC_HBM(ALGO_MS, 0, 8) QLDPC_HBM(ALGO_MS, 0, 16) QLDPC_HBM(ALGO_MS, 0, 32) QLDPC_HBM(ALGO_MS, 0, 64)
-  QLDPC_HBM(ALGO_BP, 1, 8) QLDPC_HBM(ALGO_BP, 1, 16) QLDPC_HBM(ALGO_BP, 1, 32) QLDPC_HBM(ALGO_BP, 1, 64)
-  return nullptr;
+  QLDPC_HBM(ALGO_MS, 0, 8) QLDPC_HBM(ALGO_MS, 0, 16) QLDPC_HBM(ALGO_MS, 0, 32)
+  QLDPC_HBM(ALGO_BP, 1, 8) QLDPC_HBM(ALGO_BP, 1, 16) QLDPC_HBM(ALGO_BP, 1, 32)
+  if (name) *name = algo == ALGO_MS ? "hbm_tile_kernel<0, 64, 4>" : "hbm_tile_kernel<1, 64, 4>";
+  return algo == ALGO_MS ? (const void*)&hbm_tile_kernel<ALGO_MS, 64, kHbmWaves>
+                         : (const void*)&hbm_tile_kernel<ALGO_BP, 64, kHbmWaves>;
 }
 #undef QLDPC_HBM
 

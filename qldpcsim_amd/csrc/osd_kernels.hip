@@ -25,6 +25,7 @@
 #include <stdint.h>
 
 #include "osd_kernels.h"
+#include "tuning.h"
 
 namespace qldpc {
 
@@ -59,12 +60,6 @@ __device__ __forceinline__ void spill_shot(const OsdArgs& a, long long shot, int
   if (threadIdx.x == 0) a.spill_idx[q] = (int32_t)(a.shot_base + shot);
 }
 
-#ifndef QLDPC_OSD_TIMING
-#define QLDPC_OSD_TIMING 0  // diagnostic builds: osd_block_kernel sums per-phase cycles into a.prof
-#endif
-#ifndef QLDPC_ABLATE_OSD
-#define QLDPC_ABLATE_OSD 0  // timing-only builds of osd_block_kernel: bit 0 skips phase D, bit 1 the engine
-#endif
 
 // s_getreg immediates: (size - 1) << 11 | offset << 6 | register id
 constexpr int kHwRegHwId = (31 << 11) | 4;    // HW_ID: SIMD bits 4-5, CU 8-11, SH 12, SE 13-15
@@ -282,14 +277,6 @@ __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
 //   D  every row applies its C to words w..: each update added a current
 //      pivot row = its block-start value + earlier pivot rows of the block.
 // ---------------------------------------------------------------------------
-// v_writelane_b32 (value and lane select wave-uniform; the lane select in M0:
-// gfx9's constant bus takes one SGPR per instruction); the s_nop covers the
-// SALU-write -> lane-select read hazard the compiler cannot see in inline asm
-__device__ __forceinline__ int write_lane(int old, int value, int lane) {
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 4\n\tv_writelane_b32 %0, %1, m0" : "+v"(old) : "s"(value), "s"(lane) : "m0");
-  return old;
-}
-
 __device__ __forceinline__ uint32_t opaque_u32(uint32_t x) {
   asm volatile("" : "+v"(x));
   return x;
@@ -315,7 +302,7 @@ template <int SL, int SF, bool HI>
 __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL], uint32_t (&cl)[SL],
                                           uint32_t (&ch)[SL], uint64_t (&fm)[SL], uint32_t cols, int K,
                                           int w, int lane, int& rank, int& nJ, bool& done, uint64_t& pivm,
-                                          int rankH, int m, int& pkv, int& ivv) {
+                                          int rankH, int m, int& pkv) {
   static_assert(SL <= 8, "the pivot-slot switch covers 8 slots");
   while (cols && !done) {
     // loop-carried scalars re-asserted wave-uniform: otherwise the compiler
@@ -348,7 +335,6 @@ __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL]
       if (f != 0x7fffffff) break;                   // (dependent columns: not in J)
     }
     if (f == 0x7fffffff) break;
-    const uint32_t bm = 1u << bit;
     const int fs = f >> 6, fl = f & 63;
     uint32_t plo = 0, phi = 0, pcl = 0, pch = 0;
     switch (fs) {                                   // uniform: one case runs, no select chains
@@ -367,12 +353,11 @@ __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL]
 #undef QLDPC_PIVOT_SLOT
       default: break;
     }
+    // (+ the pivot itself; the 64-bit form, (pch:pcl) ^ (1ull << K), was
+    // miscompiled in the 128-VGPR spilling instance: wrong eliminations,
+    // correct at 3 waves per SIMD without spills — tools/osd_check.py)
     if (K < 32) pcl ^= 1u << K;
     else pch ^= 1u << (K - 32);
-#ifndef QLDPC_OSD_MASKED_XOR
-#define QLDPC_OSD_MASKED_XOR 1
-#endif
-#if QLDPC_OSD_MASKED_XOR
     // Rows holding a 1 (above and below) take the pivot: x ^= p & mask with
     // mask = 0 / ~0 from the column bit (one bit-field extract), the pivot
     // row itself excluded — branch-free (v_bitop3), no exec-mask round trip
@@ -387,26 +372,13 @@ __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL]
       cl[s] ^= pcl & mk;
       ch[s] ^= pch & mk;
     }
-#else
-    const bool notme = lane != fl;
-#pragma unroll
-    for (int s = 0; s < SF; ++s) {
-      if (((HI ? hi[s] : lo[s]) & bm) != 0 && (s != fs || notme)) {   // rows holding a 1,
-        if (!HI) lo[s] ^= plo;                                         // above and below (the
-        hi[s] ^= phi;                                                  // low half is done in HI)
-        cl[s] ^= pcl;
-        ch[s] ^= pch;
-      }
-    }
-#endif
     const int wb = (HI ? 32 : 0) + bit;
     const int i = 64 * w + wb;
     pivm |= 1ull << wb;
-    // pivot K's record (compact row << 6 | column bit) and column index go to
-    // lane K of two VGPRs (no exec-masked LDS store per pivot); the block's
-    // pk / Jl / inJ entries are written once after the engine loop
-    pkv = write_lane(pkv, (f << 6) | wb, K);
-    ivv = write_lane(ivv, i, K);
+    // pivot K's record (compact row << 6 | column bit) goes to lane K of a
+    // VGPR (no exec-masked LDS store per pivot); the block's pk / Jl / inJ
+    // entries are written once after the engine loop
+    pkv = lane == K ? ((f << 6) | wb) : pkv;
     if (i != 0) ++nJ;
     ++K;
     ++rank;
@@ -422,14 +394,13 @@ template <int SL, int SFMAX, bool HI>
 __device__ __forceinline__ int block_half_n(int SF, uint32_t (&lo)[SL], uint32_t (&hi)[SL], uint32_t (&cl)[SL],
                                             uint32_t (&ch)[SL], uint64_t (&fm)[SL], uint32_t cols, int K,
                                             int w, int lane, int& rank, int& nJ, bool& done, uint64_t& pivm,
-                                            int rankH, int m, int& pkv, int& ivv) {
+                                            int rankH, int m, int& pkv) {
   if constexpr (SFMAX > 1) {
     if (SF <= SFMAX / 2)
       return block_half_n<SL, SFMAX / 2, HI>(SF, lo, hi, cl, ch, fm, cols, K, w, lane, rank, nJ, done, pivm,
-                                             rankH, m, pkv, ivv);
+                                             rankH, m, pkv);
   }
-  return block_half<SL, SFMAX, HI>(lo, hi, cl, ch, fm, cols, K, w, lane, rank, nJ, done, pivm, rankH, m, pkv,
-                                   ivv);
+  return block_half<SL, SFMAX, HI>(lo, hi, cl, ch, fm, cols, K, w, lane, rank, nJ, done, pivm, rankH, m, pkv);
 }
 
 // XOR of the 64-bit table entries tab[k] over the set bits k of v, four
@@ -481,13 +452,10 @@ __device__ __forceinline__ void osd_apply_rows(uint64_t (&R)[NW], uint64_t cm, c
 // in VGPRs; RT = rows per thread (thread t holds rows t, t + blockDim, ..):
 // with 2, a 450-row shot takes 4 waves and a CU holds 4 shots (4 engines, one
 // per SIMD) instead of 2
-#ifndef QLDPC_OSD_WPE
-#define QLDPC_OSD_WPE 4  // waves per SIMD of the two-rows-per-thread instances (3: no spills, 15 % slower)
-#endif
 template <int NW, int SL, int RT>
 __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_eu(RT == 2 ? QLDPC_OSD_WPE : 1))) osd_block_kernel(OsdArgs a) {
   // LDS: inv_perm[n] | J list [m+2] | inJ bytes [n] | emask [NW] | Wd [MR] | Cm [MR] |
-  //      PW [64][NW] | CT [64] | pkof [MR] | pidx [MR] | crow [MR] | pk [64] | misc [8] | set table
+  //      PW [64][NW] | CT [64] | pkof [MR] | pidx [MR] | crow [MR] | pk [64] | misc [16] | set table
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int m = a.m, n = a.n;
   const int B = blockDim.x, MR = RT * B;
@@ -639,41 +607,42 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
       uint64_t pivm = 0;
       // low half-word columns, then high (each loop's column order ascends)
       const int nJ0 = nJ;
-      int pkv = 0, ivv = 0;
+      int pkv = 0;
       int K = block_half_n<SL, SL, false>(SF, lo, hi, cl, ch, fm, (uint32_t)cols, 0, w, lane, rank, nJ, done,
-                                          pivm, a.rank, m, pkv, ivv);
+                                          pivm, a.rank, m, pkv);
       K = block_half_n<SL, SL, true>(SF, lo, hi, cl, ch, fm, (uint32_t)(cols >> 32), K, w, lane, rank, nJ, done,
-                                     pivm, a.rank, m, pkv, ivv);
-      // the block's J entries (column 0 is J's first entry from the start)
-      const int z = (K > 0 && __builtin_amdgcn_readlane(ivv, 0) == 0) ? 1 : 0;
-      if (lane < K) {
-        pk[lane] = pkv;
-        if (ivv != 0) {
-          Jl[nJ0 + lane - z] = ivv;
-          inJ[ivv] = 1;
-        }
-      }
+                                     pivm, a.rank, m, pkv);
 #pragma unroll
       for (int s = 0; s < SL; ++s) {
         const int cp = 64 * s + lane;
         if (cp < F) Cm[crow[cp]] = ((uint64_t)ch[s] << 32) | cl[s];
       }
-      // (one wave: its LDS accesses complete in order, so these reads see
+      // (one wave: its LDS accesses complete in order, so the reads below see
       // the writes above)
-      if (lane < K) {
-        const int e = pkv;
-        const int row = crow[e >> 6];
-        CT[e & 63] = Cm[row] ^ (1ull << lane);        // reduced pivot k = its own row + C
-        pkof[row] = 64 * w + lane;
-        pidx[row] = rank0 + lane;                     // REF moves the k-th pivot row to row k
-      }
-      if (lane == 0) {
-        misc[0] = nJ;
-        misc[1] = rank;
-        misc[4] = done;
-        misc[5] = K;
-        misc[6] = (int)(uint32_t)pivm;
-        misc[7] = (int)(uint32_t)(pivm >> 32);
+      {
+        // the block's J entries (column 0 is J's first entry from the start)
+        const int ivv = 64 * w + (pkv & 63);
+        const int z = (K > 0 && __builtin_amdgcn_readlane(ivv, 0) == 0) ? 1 : 0;
+        if (lane < K) {
+          pk[lane] = pkv;
+          if (ivv != 0) {
+            Jl[nJ0 + lane - z] = ivv;
+            inJ[ivv] = 1;
+          }
+          const int e = pkv;
+          const int row = crow[e >> 6];
+          CT[e & 63] = Cm[row] ^ (1ull << lane);      // reduced pivot k = its own row + C
+          pkof[row] = 64 * w + lane;
+          pidx[row] = rank0 + lane;                   // REF moves the k-th pivot row to row k
+        }
+        if (lane == 0) {
+          misc[0] = nJ;
+          misc[1] = rank;
+          misc[4] = done;
+          misc[5] = K;
+          misc[6] = (int)(uint32_t)pivm;
+          misc[7] = (int)(uint32_t)(pivm >> 32);
+        }
       }
     }
     QLDPC_TICK(2);

@@ -14,6 +14,9 @@
 // Arguments: syndromes uint8 [B, m] (one byte per check) or int64
 // [B, ceil(m/64)] (bit-packed words) on a HIP device; H [m, n] and the
 // schedule (layer_ptr [L+1], layer_rows, int32 or int64) as CPU tensors.
+// The cache is keyed by a 128-bit hash of H's own bytes (dtype and shape
+// included), so a call with a cached H reads it once and copies nothing;
+// torch.ops.qldpc.release() synchronizes the devices and frees the cache.
 // Errors as decode_batch / the reference: ValueError for shapes / options
 // (and for CPU syndromes: there is no CPU path), IndexError for layer rows out
 // of range (decoders.py:156, :250), RuntimeError for HIP failures.
@@ -22,6 +25,7 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/library.h>
 
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <string>
@@ -38,7 +42,37 @@ struct CodeEntry {
   std::map<std::vector<int32_t>, qldpc_schedule*> scheds;   // key: layer_ptr ++ layer_rows
 };
 std::mutex g_mu;
-std::map<std::pair<int, std::string>, CodeEntry> g_codes;  // (device, shape + H bytes)
+struct CodeKey {
+  int dev;
+  int64_t m, n;
+  int dtype;
+  uint64_t h0, h1;   // two 64-bit hashes of H's bytes (different seeds)
+  bool operator<(const CodeKey& o) const {
+    return std::tie(dev, m, n, dtype, h0, h1) < std::tie(o.dev, o.m, o.n, o.dtype, o.h0, o.h1);
+  }
+};
+std::map<CodeKey, CodeEntry> g_codes;
+
+// four-lane multiply-rotate hash (xxh64's round) over the bytes: ~10 GB/s,
+// so a cached H costs one read instead of a mod-2 copy into a string key
+uint64_t hash_bytes(const unsigned char* p, size_t len, uint64_t seed) {
+  constexpr uint64_t P1 = 11400714785074694791ull, P2 = 14029467366897019727ull, P3 = 1609587929392839161ull;
+  auto rotl = [](uint64_t x, int r) { return (x << r) | (x >> (64 - r)); };
+  uint64_t a[4] = {seed + P1 + P2, seed + P2, seed, seed - P1};
+  size_t i = 0;
+  for (; i + 32 <= len; i += 32)
+    for (int k = 0; k < 4; ++k) {
+      uint64_t w;
+      memcpy(&w, p + i + 8 * k, 8);
+      a[k] = rotl(a[k] + w * P2, 31) * P1;
+    }
+  uint64_t h = rotl(a[0], 1) + rotl(a[1], 7) + rotl(a[2], 12) + rotl(a[3], 18) + len;
+  for (; i < len; ++i) h = rotl(h ^ (p[i] * P3), 11) * P1;
+  h ^= h >> 33;
+  h *= P2;
+  h ^= h >> 29;
+  return h;
+}
 
 void check(int rc) {
   if (rc == QLDPC_OK) return;
@@ -73,10 +107,11 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> decode_hip(
   const int dev = s.get_device();
 
   // graph and schedule, built once per (device, H) / layer partition
-  const at::Tensor Hb = H.remainder(2).to(at::kByte).contiguous();          // load_matrix's (mat % 2)
-  std::string key(reinterpret_cast<const char*>(&m), sizeof m);
-  key.append(reinterpret_cast<const char*>(&n), sizeof n);
-  key.append(reinterpret_cast<const char*>(Hb.data_ptr<uint8_t>()), (size_t)(m * n));
+  const at::Tensor Hc = H.contiguous();
+  const size_t hbytes = (size_t)Hc.numel() * Hc.element_size();
+  const auto* hp = static_cast<const unsigned char*>(Hc.data_ptr());
+  const CodeKey key{dev, m, n, (int)Hc.scalar_type(), hash_bytes(hp, hbytes, 0x51ED2701ull),
+                    hash_bytes(hp, hbytes, 0x2545F4914F6CDD1Dull)};
   std::vector<int32_t> lp = as_i32(layer_ptr, "layer_ptr"), lr = as_i32(layer_rows, "layer_rows");
   TORCH_CHECK_VALUE(lp.size() >= 2 && lp.front() == 0 && (size_t)lp.back() == lr.size(),
                     "qldpc::decode: layer_ptr must run from 0 to len(layer_rows)");
@@ -87,8 +122,11 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> decode_hip(
   qldpc_schedule* sched = nullptr;
   {
     std::lock_guard<std::mutex> lk(g_mu);
-    CodeEntry& ce = g_codes[{dev, key}];
-    if (!ce.code) check(qldpc_code_create(Hb.data_ptr<uint8_t>(), (int)m, (int)n, &ce.code));
+    CodeEntry& ce = g_codes[key];
+    if (!ce.code) {
+      const at::Tensor Hb = Hc.remainder(2).to(at::kByte).contiguous();     // load_matrix's (mat % 2)
+      check(qldpc_code_create(Hb.data_ptr<uint8_t>(), (int)m, (int)n, &ce.code));
+    }
     code = ce.code;
     auto it = ce.scheds.find(skey);
     if (it == ce.scheds.end()) {
@@ -121,12 +159,26 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> decode_cpu(
                     syn.device(), ")");
 }
 
+// Frees every cached graph and schedule (their device tables and HBM
+// workspaces) after the devices holding them have finished all work.
+void release() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (auto& kv : g_codes) {
+    const c10::hip::HIPGuardMasqueradingAsCUDA guard(c10::Device(c10::DeviceType::CUDA, kv.first.dev));
+    TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "qldpc::release: device synchronize failed");
+    for (auto& s : kv.second.scheds) qldpc_schedule_destroy(s.second);
+    qldpc_code_destroy(kv.second.code);
+  }
+  g_codes.clear();
+}
+
 }  // namespace
 
 TORCH_LIBRARY(qldpc, m) {
   m.def("decode(Tensor syndromes, Tensor H, Tensor layer_ptr, Tensor layer_rows, float p, int max_iter, "
         "str algo='MS', float beta=0.75, float eps=1e-09, bool want_post=False, bool ehat_bits=False) "
         "-> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("release() -> ()", &release);
 }
 TORCH_LIBRARY_IMPL(qldpc, CUDA, m) { m.impl("decode", &decode_hip); }   // (HIP devices dispatch as CUDA)
 TORCH_LIBRARY_IMPL(qldpc, CPU, m) { m.impl("decode", &decode_cpu); }

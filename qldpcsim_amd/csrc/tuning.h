@@ -1,0 +1,51 @@
+// tuning.h — compile-time knobs of the HIP kernels, all in one place.
+//
+// The shipping build uses the measured defaults below (DESIGN.md cites the
+// A/B that chose each). Experiment builds (tools/build_variants.sh) may set
+// any of them with -D, but only together with -DQLDPC_EXPERIMENTS: a knob
+// defined without it is a build error, so no ablation or diagnostic setting
+// reaches the product library by accident. Runtime kernel-family choices are
+// library options (qldpc_set_option, include/qldpc_decoder.h), not knobs.
+#pragma once
+
+#if !defined(QLDPC_EXPERIMENTS) &&                                                                   \
+    (defined(QLDPC_ABLATE) || defined(QLDPC_ABLATE_L) || defined(QLDPC_ABLATE_OSD) ||               \
+     defined(QLDPC_OSD_TIMING) || defined(QLDPC_VN_PAIR) || defined(QLDPC_FLOOD_WPE) ||             \
+     defined(QLDPC_VN_H) || defined(QLDPC_HBM_WAVES) || defined(QLDPC_HBM_UC) ||                    \
+     defined(QLDPC_OSD_WPE))
+#error "kernel tuning knobs are for experiment builds: add -DQLDPC_EXPERIMENTS"
+#endif
+
+// knock-outs for timing attribution (experiment builds only)
+#ifndef QLDPC_ABLATE
+#define QLDPC_ABLATE 0       // flooding decode_kernel: 1 = skip VN, 2 = skip CN
+#endif
+#ifndef QLDPC_ABLATE_L
+#define QLDPC_ABLATE_L 0     // ms_layered_kernel: bit 0 skips CN, bit 1 VN, bit 2 the filter
+#endif
+#ifndef QLDPC_ABLATE_OSD
+#define QLDPC_ABLATE_OSD 0   // osd_block_kernel: bit 0 skips phase D, bit 1 the engine
+#endif
+#ifndef QLDPC_OSD_TIMING
+#define QLDPC_OSD_TIMING 0   // osd_block_kernel sums per-phase cycles into OsdArgs::prof (option osd_prof)
+#endif
+
+// measured defaults
+#ifndef QLDPC_VN_PAIR
+#define QLDPC_VN_PAIR 1      // ms_flood_kernel VN: two 64-variable chunks per trip
+#endif
+#ifndef QLDPC_FLOOD_WPE
+#define QLDPC_FLOOD_WPE 3    // ms_flood_kernel: waves per SIMD the register budget targets (KC <= 4)
+#endif
+#ifndef QLDPC_VN_H
+#define QLDPC_VN_H 4         // ms_layered_kernel: variables per lane on layers of > 128 adjacent variables
+#endif
+#ifndef QLDPC_HBM_WAVES
+#define QLDPC_HBM_WAVES 4    // hbm_tile_kernel: waves per 64-slot tile (kernel names spell out 4)
+#endif
+#ifndef QLDPC_HBM_UC
+#define QLDPC_HBM_UC 1       // hbm_tile_kernel: checks per load step (1: 16 waves per CU; 2, 4 slower)
+#endif
+#ifndef QLDPC_OSD_WPE
+#define QLDPC_OSD_WPE 4      // osd_block_kernel, two rows per thread: waves per SIMD (3: no spills, slower)
+#endif

@@ -11,9 +11,12 @@ plus the batched entry point the simulator uses, `decode_batch`, which decodes
 many syndromes of one matrix in one kernel launch.
 
 All decoding runs through the HIP kernels (libqldpc_hip.so via the C ABI);
-there is no CPU fallback. OSD is host C++ (it runs only for non-converged
-shots), fed the reliability order computed with NumPy exactly as
-decoders.py:320-325 does.
+there is no CPU fallback. OSD of the non-converged shots runs on the device
+(osd_kernels.hip: the reliability order, certified against NumPy's tie
+breaking, and a block GF(2) elimination); shots whose order the device
+cannot certify get NumPy's own order (decoders.py:320-325) on the host and
+the device elimination again. `OSDdec` / `apply_osd` are the single-shot and
+host entry points (host C++ elimination).
 
 Deviations from the reference (documented in DESIGN.md §6):
   * layers=None means flooding (the reference raises AttributeError on
@@ -23,12 +26,14 @@ Deviations from the reference (documented in DESIGN.md §6):
   * The min-sum "leak" case (a v2c message exactly 0.0, App. A.1.6) is
     flagged (FLAG_MIN_ZERO) but not emulated.
 """
+import contextlib
+import os
 from dataclasses import dataclass
 from typing import Optional
 
 import numpy as np
 
-from . import _lib
+from . import _lib, hostcores
 from .schedule import pack_layers
 
 __all__ = ["MS_decoder", "BP_decoder", "OSDdec", "decode_batch", "DecodeResult", "osd_perm", "pack_bits",
@@ -192,8 +197,7 @@ def osd_perms(post, nthreads=None):
             out[r0:r0 + 64] = np.argsort(t, axis=1)
         return out
 
-    import os
-    nthreads = nthreads or min(16, os.cpu_count() or 1)
+    nthreads = nthreads or hostcores.rank_cores()
     if post.shape[0] < 256 or nthreads <= 1:
         return one(post)
     # a persistent pool (starting 16 threads per call had cost ~4 ms, more than
@@ -258,20 +262,45 @@ def apply_osd_device_many(items, order, stream=None):
     return [r.ehat for _, _, r in items]
 
 
+# Where the OSD reliability order comes from (decoders.py:320-325):
+#   device_min  fewest non-converged shots of one decode for which the order
+#               is computed on the device. Below it NumPy orders them on the
+#               host in one pass: few shots cost the host little, the device
+#               order would add a round trip (status back, then the host pass
+#               anyway for the tie-holding shots), and at low p most OSD shots
+#               carry saturated posteriors, whose exact key ties send them to
+#               the host regardless (LP118_2 MS-L p = 0.05: 735 of 738);
+#   host_order  NumPy's order for every OSD shot (A/B reference).
+# Read once at import from QLDPC_OSD_DEVICE_MIN / QLDPC_OSD_HOST_ORDER (tools
+# start one process per setting); set_osd_policy / osd_policy change it.
+OSD_POLICY = {"device_min": int(os.environ.get("QLDPC_OSD_DEVICE_MIN", "4096")),
+              "host_order": os.environ.get("QLDPC_OSD_HOST_ORDER", "") == "1"}
+
+
+def set_osd_policy(device_min=None, host_order=None):
+    if device_min is not None:
+        OSD_POLICY["device_min"] = int(device_min)
+    if host_order is not None:
+        OSD_POLICY["host_order"] = bool(host_order)
+
+
+@contextlib.contextmanager
+def osd_policy(**kw):
+    """`with osd_policy(device_min=1): ...` — the previous policy comes back after."""
+    old = dict(OSD_POLICY)
+    try:
+        set_osd_policy(**kw)
+        yield
+    finally:
+        OSD_POLICY.update(old)
+
+
 def _host_order_only():
-    import os
-    return os.environ.get("QLDPC_OSD_HOST_ORDER", "") == "1"
+    return OSD_POLICY["host_order"]
 
 
 def _device_order_min():
-    """Fewest non-converged shots of one decode for which the reliability order
-    is computed on the device. Below it NumPy orders them on the host in one
-    pass: few shots cost the host little, the device order would add a round
-    trip (status back, then the host pass anyway for the tie-holding shots),
-    and at low p most OSD shots carry saturated posteriors, whose exact key
-    ties send them to the host regardless (LP118_2 MS-L p = 0.05: 735 of 738)."""
-    import os
-    return int(os.environ.get("QLDPC_OSD_DEVICE_MIN", "4096"))
+    return OSD_POLICY["device_min"]
 
 
 def _on_stream(stream):
@@ -287,9 +316,12 @@ def _on_stream(stream):
 
 def release_workspaces():
     """Free the grow-only device OSD spill workspaces and pinned staging
-    buffers (they are reused across batches while a sweep runs)."""
+    buffers (they are reused across batches while a sweep runs), and the HBM
+    workspaces of every cached schedule (hbm_tile_kernel's message state:
+    up to half the free device memory per schedule, kept between launches)."""
     _DEVBUF.clear()
     _PINNED.clear()
+    _lib.release_hbm_workspaces()
 
 
 def osd_device_stage(items, stream=None, slot0=0, order=0):
@@ -299,7 +331,7 @@ def osd_device_stage(items, stream=None, slot0=0, order=0):
     whose result the device order decides, with its status copied into a
     pinned host buffer. Shots that need NumPy's order (status 2) are finished
     by osd_device_finish. `slot0` selects the pinned buffer set (pipelined
-    callers alternate). QLDPC_OSD_HOST_ORDER=1 (A/B only) or n > 2048 sends
+    callers alternate). OSD_POLICY["host_order"] (A/B only) or n > 2048 sends
     every shot through NumPy's order, as osd_perms computes it."""
     staged = []
     with _on_stream(stream):
@@ -505,7 +537,7 @@ def osd_status_raise(flags):
         raise IndexError("OSD: column basis search ran past the last column")
 
 
-def apply_osd(H, syn, ehat, post, flags, order, nthreads=0):
+def apply_osd(H, syn, ehat, post, flags, order, nthreads=None):
     """OSD post-step for every non-converged row (decoders.py:179-180, :287-288).
 
     ehat (uint8 [B, n]) is updated in place.
@@ -519,7 +551,7 @@ def apply_osd(H, syn, ehat, post, flags, order, nthreads=0):
     sub_e = np.ascontiguousarray(ehat[idx], dtype=np.uint8)
     _lib.check(_lib.lib.qldpc_osd_decode_batch(code.handle, idx.size, _lib.ptr(sub_syn),
                                                _lib.ptr(perms), int(order), _lib.ptr(sub_e),
-                                               int(nthreads)))
+                                               int(nthreads or hostcores.rank_cores())))
     ehat[idx] = sub_e
     return ehat
 

@@ -16,6 +16,31 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run on the GPU box")
 
 
+@pytest.fixture
+def qopt():
+    """Set library options (qldpc_set_option) for one test: qopt(force_hbm=1, ...);
+    every option touched gets its previous value back afterwards."""
+    from qldpcsim_amd import _lib
+    saved = {}
+
+    def set_(**kw):
+        for k, v in kw.items():
+            saved.setdefault(k, _lib.get_option(k))
+            _lib.set_option(k, v)
+    yield set_
+    for k, v in saved.items():
+        _lib.set_option(k, v)
+
+
+@pytest.fixture
+def osdpol():
+    """Set the OSD reliability-order policy (decoders.OSD_POLICY) for one test."""
+    from qldpcsim_amd import decoders
+    old = dict(decoders.OSD_POLICY)
+    yield decoders.set_osd_policy
+    decoders.OSD_POLICY.update(old)
+
+
 def golden_files(pattern=""):
     return sorted(os.path.join(GOLDEN, f) for f in os.listdir(GOLDEN)
                   if f.endswith(".npz") and pattern in f)

@@ -31,6 +31,24 @@ def test_every_declared_symbol_is_exported():
         assert hasattr(lib, name), name
 
 
+def test_library_options_roundtrip_and_unknown_names():
+    """qldpc_set_option / qldpc_get_option: every documented name with its
+    default, set / restore through the context manager, ValueError for an
+    unknown name (the library itself never reads the environment)."""
+    defaults = {"force_hbm": 0, "flood_generic": 0, "layered_generic": 0, "ms_lanes_per_check": 0, "bp_wave": 0,
+                "bp_lg": 1, "bp_team_w": 0, "static_sched": 0, "waves_per_wg": 0, "wg_per_cu": 0,
+                "osd_column": 0, "osd_tickets": 1, "osd_prof": 0}
+    for k, v in defaults.items():
+        assert _lib.get_option(k) == v, k
+    with _lib.options(force_hbm=1, bp_team_w=8):
+        assert _lib.get_option("force_hbm") == 1 and _lib.get_option("bp_team_w") == 8
+    assert _lib.get_option("force_hbm") == 0 and _lib.get_option("bp_team_w") == 0
+    with pytest.raises(ValueError, match="unknown option"):
+        _lib.set_option("no_such_option", 1)
+    src = open(os.path.join(ROOT, "qldpcsim_amd", "csrc", "capi.cpp")).read()
+    assert "getenv" not in src
+
+
 def test_version_and_device_count():
     assert b"gfx950" in _lib.lib.qldpc_version()
     assert _lib.device_count() >= 0

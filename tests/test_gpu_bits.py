@@ -7,7 +7,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-KERNEL_ENVS = {"fast": {}, "generic": {"QLDPC_NO_REGTAB": "1", "QLDPC_NO_LAYERED_FAST": "1"}}
+KERNEL_ENVS = {"fast": {}, "generic": {"flood_generic": 1, "layered_generic": 1}}   # library options
 
 
 @pytest.mark.parametrize("env", sorted(KERNEL_ENVS))
@@ -15,12 +15,11 @@ KERNEL_ENVS = {"fast": {}, "generic": {"QLDPC_NO_REGTAB": "1", "QLDPC_NO_LAYERED
     ("LP118_0", "MS", "F"), ("LP118_2", "MS", "L"), ("LP04_0", "MS", "S"), ("steane", "MS", "F"),
     ("LP118_0", "BP", "F"), ("LP118_2", "BP", "L"), ("bicycle", "MS", "L"), ("shor", "BP", "F"),
 ])
-def test_bit_packed_decode_equals_bytes(code, algo, sched, env, monkeypatch):
+def test_bit_packed_decode_equals_bytes(code, algo, sched, env, qopt):
     import torch
     from qldpcsim_amd import _lib, codes, decoders, schedule
     Hx, Hz = codes.load_code(code)
-    for k, v in KERNEL_ENVS[env].items():
-        monkeypatch.setenv(k, v)
+    qopt(**KERNEL_ENVS[env])
     lx, _ = schedule.select_layers(Hx, Hz, sched)
     lp, lr = schedule.pack_layers(lx, Hz.shape[0])
     _lib.code_for(Hz, 0)._sched.clear()

@@ -2,7 +2,7 @@
 cannot hold (per-half-shot state beyond a CU's LDS, tables past 16 bits)
 decode through it automatically, and it equals the oracle bit for bit —
 the reference's arithmetic (decoders.py:110-182, :189-290) at any size.
-QLDPC_FORCE_HBM=1 routes the bundled codes through it too, so it is also
+The library option force_hbm routes the bundled codes through it too, so it is also
 pinned against the reference's golden vectors."""
 import numpy as np
 import pytest
@@ -82,13 +82,13 @@ def test_code_past_16_bit_tables_decodes():
 
 
 @pytest.mark.parametrize("algo", ["MS", "BP"])
-def test_forced_hbm_matches_reference_goldens(algo, monkeypatch):
-    """QLDPC_FORCE_HBM=1: the bundled codes' golden cases (every schedule,
+def test_forced_hbm_matches_reference_goldens(algo, qopt):
+    """Option force_hbm: the bundled codes' golden cases (every schedule,
     the 100-iteration BP set included) through the HBM kernel reproduce the
     reference bit for bit."""
     import torch
     from qldpcsim_amd import _lib, decoders
-    monkeypatch.setenv("QLDPC_FORCE_HBM", "1")
+    qopt(force_hbm=1)
     n = 0
     for c, a in golden_cases():
         if "raises" in c or c["algo"] != algo or c["code"] not in ("LP04_0", "LP118_0", "LP118_2", "steane"):
@@ -106,7 +106,7 @@ def test_forced_hbm_matches_reference_goldens(algo, monkeypatch):
     assert n > 300
 
 
-def test_forced_hbm_early_stopping_batch_equals_lds_kernels(monkeypatch):
+def test_forced_hbm_early_stopping_batch_equals_lds_kernels(qopt):
     """Lane recycling over a large batch of decodes of very different lengths
     (p = 0.04 channel + fixed-work syndromes, LP118_0 layered MS): the HBM
     kernel equals the default LDS kernel on every half-shot."""
@@ -120,7 +120,7 @@ def test_forced_hbm_early_stopping_batch_equals_lds_kernels(monkeypatch):
     syn = syn[np.random.default_rng(1).permutation(len(syn))]
     s = torch.as_tensor(syn, device="cuda")
     ref = decoders.decode_batch(Hz, s, 0.04 / 3, 40, algo="MS", want_post=True, layer_ptr=lp, layer_rows=lr)
-    monkeypatch.setenv("QLDPC_FORCE_HBM", "1")
+    qopt(force_hbm=1)
     assert _lib.kernel_name(Hz, lp, lr, "MS") == "hbm_tile_kernel<0, 8, 4>"
     got = decoders.decode_batch(Hz, s, 0.04 / 3, 40, algo="MS", want_post=True, layer_ptr=lp, layer_rows=lr)
     torch.cuda.synchronize()
@@ -131,7 +131,7 @@ def test_forced_hbm_early_stopping_batch_equals_lds_kernels(monkeypatch):
 
 
 @pytest.mark.parametrize("B", [1, 63, 65, 1000])
-def test_forced_hbm_ragged_batches_and_edge_cases(B, monkeypatch):
+def test_forced_hbm_ragged_batches_and_edge_cases(B, qopt):
     """Batches that do not fill a 64-slot tile (1, 63, 65, 1000 half-shots),
     all-zero syndromes (converged after the first iteration), max_iter = 1,
     bit-packed I/O: the HBM kernel equals the LDS kernels on every output."""
@@ -146,10 +146,10 @@ def test_forced_hbm_ragged_batches_and_edge_cases(B, monkeypatch):
         lp, lr = schedule.pack_layers(lx, Hz.shape[0])
         for algo, it in (("MS", 1), ("MS", 30), ("BP", 1), ("BP", 12)):
             s = decoders.pack_bits(torch.as_tensor(syn, device="cuda"))
-            monkeypatch.delenv("QLDPC_FORCE_HBM", raising=False)
+            qopt(force_hbm=0)
             ref = decoders.decode_batch(Hz, s, 0.03, it, algo=algo, want_post=True, layer_ptr=lp,
                                         layer_rows=lr, ehat_bits=True)
-            monkeypatch.setenv("QLDPC_FORCE_HBM", "1")
+            qopt(force_hbm=1)
             got = decoders.decode_batch(Hz, s, 0.03, it, algo=algo, want_post=True, layer_ptr=lp,
                                         layer_rows=lr, ehat_bits=True)
             torch.cuda.synchronize()
@@ -157,3 +157,47 @@ def test_forced_hbm_ragged_batches_and_edge_cases(B, monkeypatch):
             assert torch.equal(got.flags, ref.flags)
             assert torch.equal(got.post.view(torch.int64), ref.post.view(torch.int64))
             assert (got.iters[::3] == 1).all()                    # zero syndromes: converged at once
+
+
+@pytest.mark.parametrize("algo", ["MS", "BP"])
+def test_forced_hbm_non_partition_schedule(algo, qopt):
+    """A schedule that is not a partition of the rows (row 5 in two layers,
+    row 10 in none): the HBM kernel's state-initialising path (hbm_lazy = 0:
+    no first-layer tables) against the oracle and against the LDS kernels,
+    max_iter 1 and 20, 200 half-shots (64-slot tiles recycled)."""
+    import torch
+    from qldpcsim_amd import _lib, codes, decoders, schedule
+    Hx, Hz = codes.load_code("LP04_0")
+    layers = [np.asarray(l) for l in schedule.layerize(Hx)]
+    layers[-1] = np.append(layers[-1], 5)                   # row 5 again in the last layer
+    layers = [l[l != 10] for l in layers]                   # row 10 in no layer
+    assert any(5 in l for l in layers[:-1]) and not any(10 in l for l in layers)
+    lp, lr = schedule.pack_layers(layers, Hz.shape[0])
+    syn = np.concatenate([_syndromes(Hz, 150, 0.05, 21),
+                          np.random.default_rng(22).integers(0, 2, (50, Hz.shape[0]), dtype=np.uint8)])
+    for it in (1, 20):
+        qopt(force_hbm=0)
+        ref = decoders.decode_batch(Hz, torch.as_tensor(syn, device="cuda"), 0.05 / 3, it, algo=algo,
+                                    want_post=True, layer_ptr=lp, layer_rows=lr)
+        qopt(force_hbm=1)
+        assert _lib.kernel_name(Hz, lp, lr, algo).startswith("hbm_tile_kernel<")
+        got = _check(Hz, syn, algo, 0.05 / 3, it, lp, lr)
+        assert torch.equal(got.iters, ref.iters) and torch.equal(got.ehat, ref.ehat)
+        assert torch.equal(got.post.view(torch.int64), ref.post.view(torch.int64))
+
+
+@pytest.mark.parametrize("algo,sched", [("MS", "F"), ("MS", "L"), ("BP", "F"), ("BP", "L")])
+def test_rows_wider_than_64_edges_decode(algo, sched):
+    """Row degree 100 (the reference's decoders take any H): the HBM kernel's
+    two-pass check node for rows past its 64-edge registers, against the
+    oracle bit for bit on converging and fixed-work syndromes, 80 half-shots
+    (64-slot tiles recycled)."""
+    from qldpcsim_amd import _lib, schedule
+    H = _regular_code(1200, 5, 100, 7)
+    assert H.sum(axis=1).max() > 64
+    layers = [np.arange(H.shape[0])] if sched == "F" else schedule.layerize(H)
+    lp, lr = schedule.pack_layers(layers, H.shape[0])
+    assert _lib.kernel_name(H, lp, lr, algo) == f"hbm_tile_kernel<{0 if algo == 'MS' else 1}, 64, 4>"
+    syn = np.concatenate([_syndromes(H, 60, 0.004, 3), np.random.default_rng(4).integers(0, 2, (20, H.shape[0]),
+                                                                                         dtype=np.uint8)])
+    _check(H, syn, algo, 0.004, 8 if algo == "BP" else 15, lp, lr)

@@ -26,9 +26,11 @@ def _gpu_osd(H, syn, e, post, order):
 @pytest.mark.parametrize("order", [0, 1, 2, 4])
 def test_gpu_osd_matches_host_osd(code, order):
     from qldpcsim_amd import _lib, codes, decoders
+    import zlib
     Hx, Hz = codes.load_code(code)
-    rng = np.random.default_rng(hash((code, order)) % 2**32)
-    for H in (Hx, Hz):
+    # a reproducible seed per case (Python's str hash is salted per process)
+    rng = np.random.default_rng(zlib.crc32(f"{code}-{order}".encode()))
+    for H in (Hx, Hz, Hx, Hz):
         k = 48
         syn = rng.integers(0, 2, (k, H.shape[0])).astype(np.uint8)
         # half consistent syndromes (valid errors), half arbitrary (inconsistent)
@@ -131,7 +133,7 @@ def test_device_order_equals_numpy_below_tiepos(code, p):
 
 
 @pytest.mark.parametrize("code,p,order", [("LP118_2", 0.1, 0), ("LP118_0", 0.08, 1), ("LP04_0", 0.12, 4)])
-def test_ordered_device_osd_equals_numpy_ordered_osd(code, p, order, monkeypatch):
+def test_ordered_device_osd_equals_numpy_ordered_osd(code, p, order, osdpol):
     """qldpc_osd_device_ordered gives the NumPy-ordered result on every shot it
     decides (status 0) and leaves the rest untouched (status 2); the
     apply_osd_device path (device order + host fallback) equals the host OSD
@@ -157,7 +159,7 @@ def test_ordered_device_osd_equals_numpy_ordered_osd(code, p, order, monkeypatch
     np.testing.assert_array_equal(got[~ok], e[~ok])
     assert ok.mean() > 0.5, ok.mean()
     # the full device path with the host fallback (device order at any count)
-    monkeypatch.setenv("QLDPC_OSD_DEVICE_MIN", "1")
+    osdpol(device_min=1)
     res = decoders.DecodeResult(d(e, np.uint8), torch.zeros(k, dtype=torch.int32, device="cuda"), p_d,
                                 torch.zeros(k, dtype=torch.int32, device="cuda"))
     decoders.apply_osd_device(H, s_d, res, order)
@@ -165,9 +167,9 @@ def test_ordered_device_osd_equals_numpy_ordered_osd(code, p, order, monkeypatch
 
 
 @pytest.mark.parametrize("code", ["LP04_0", "LP118_2", "bicycle"])
-def test_block_kernel_matches_column_kernel(code, monkeypatch):
+def test_block_kernel_matches_column_kernel(code, qopt):
     """The block elimination (pivots by row index, default) and the exact-REF
-    column kernel (QLDPC_OSD_KERNEL=column) agree shot for shot, on consistent
+    column kernel (option osd_column) agree shot for shot, on consistent
     and inconsistent syndromes (the latter take the column kernel's second
     pass inside the block path)."""
     from qldpcsim_amd import codes
@@ -181,9 +183,9 @@ def test_block_kernel_matches_column_kernel(code, monkeypatch):
     e0 = (post < 0).astype(np.uint8)
     for order in (0, 1):
         blk, sb = _gpu_osd(Hx, syn, e0, post, order)
-        monkeypatch.setenv("QLDPC_OSD_KERNEL", "column")
+        qopt(osd_column=1)
         col, sc = _gpu_osd(Hx, syn, e0, post, order)
-        monkeypatch.delenv("QLDPC_OSD_KERNEL")
+        qopt(osd_column=0)
         assert np.all(sb == 0) and np.all(sc == 0)
         np.testing.assert_array_equal(blk, col)
 
@@ -298,14 +300,14 @@ def test_ordered_osd_spill_matches_status():
     np.testing.assert_array_equal(sp_post[:c].cpu().numpy(), q[idx])
 
 
-def test_apply_osd_device_on_explicit_stream_and_rejects_packed_formats(monkeypatch):
+def test_apply_osd_device_on_explicit_stream_and_rejects_packed_formats(osdpol):
     """apply_osd_device(..., stream=s) queues every kernel, copy and event on
     `s` (same result as torch's current stream), and refuses bit-packed
     decodes (int64 word syndromes / ehat_bits) instead of letting the byte-
     wide OSD kernels read and write past them."""
     import torch
     from qldpcsim_amd import decoders
-    monkeypatch.setenv("QLDPC_OSD_DEVICE_MIN", "1")
+    osdpol(device_min=1)
     H, syn, e, post = _decoded_posteriors("LP118_2", 0.1, 600, 30, 13)
     k = len(syn)
     d = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a, dt), device="cuda")  # noqa: E731
@@ -328,7 +330,7 @@ def test_apply_osd_device_on_explicit_stream_and_rejects_packed_formats(monkeypa
 
 @pytest.mark.parametrize("device_min", ["1", "4096"])    # device reliability order / host order
 @pytest.mark.parametrize("order", [0, 1])
-def test_device_osd_pipeline_matches_reference_at_configs3(order, device_min, monkeypatch):
+def test_device_osd_pipeline_matches_reference_at_configs3(order, device_min, osdpol):
     """configs[3]'s setting from the reference itself (tests/golden/
     ms_LP118_2_osd50.npz: LP118_2 MS layered, 50 iterations, p = 0.1): the
     device decode reproduces the reference's iterations and posteriors, then
@@ -339,7 +341,7 @@ def test_device_osd_pipeline_matches_reference_at_configs3(order, device_min, mo
     import torch
     from conftest import golden_cases, half_matrix
     from qldpcsim_amd import decoders
-    monkeypatch.setenv("QLDPC_OSD_DEVICE_MIN", device_min)
+    osdpol(device_min=int(device_min))
     n_osd = fallback = 0
     for c, a in golden_cases("_osd50"):
         H = half_matrix(c)
@@ -359,3 +361,27 @@ def test_device_osd_pipeline_matches_reference_at_configs3(order, device_min, mo
     assert n_osd >= 64, n_osd
     if device_min == "1":
         assert 0 < fallback < n_osd, (fallback, n_osd)    # ties sent some shots to NumPy's order
+
+
+def test_gpu_osd_refuses_large_code_fast():
+    """A code past the GPU OSD's limits (m > 1024) is refused with
+    NotImplementedError before the host builds its rank / column bit-vectors
+    (a 3000 x 6000 H: the refusal must not pay an O(m n^2 / 64) host rank)."""
+    import time
+    import torch
+    from qldpcsim_amd import _lib
+    rng = np.random.default_rng(8)
+    m, n = 3000, 6000
+    H = np.zeros((m, n), np.uint8)
+    H[rng.integers(0, m, 6 * n), np.repeat(np.arange(n), 6)] = 1
+    code = _lib.code_for(H, 0)
+    k = 4
+    d = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a, dt), device="cuda")  # noqa: E731
+    syn, e = d(np.zeros((k, m)), np.uint8), d(np.zeros((k, n)), np.uint8)
+    st = torch.empty(k, dtype=torch.int32, device="cuda")
+    perm = torch.arange(n, dtype=torch.int32, device="cuda").repeat(k, 1)   # a valid order, should it run
+    t0 = time.perf_counter()
+    with pytest.raises(NotImplementedError):
+        _lib.check(_lib.lib.qldpc_osd_device(code.handle, k, syn.data_ptr(), perm.data_ptr(), 0, e.data_ptr(),
+                                             st.data_ptr(), None))
+    assert time.perf_counter() - t0 < 0.5

@@ -247,19 +247,19 @@ KERNELS = ["G1", "G2", "G4", "G8", "generic", "default"]
 
 @pytest.mark.parametrize("code", ["LP118_2", "LP118_0", "LP04_0"])
 @pytest.mark.parametrize("kernel", KERNELS)
-def test_ms_layered_kernels_match_oracle(dec, kernel, code, monkeypatch):
+def test_ms_layered_kernels_match_oracle(dec, kernel, code, qopt):
     """Every layered MS kernel shape against the oracle, bit for bit, with
     fixed-work and channel syndromes mixed in one batch: ms_layered_kernel at
-    every lanes-per-check width G (QLDPC_MS_LANES_PER_CHECK), the default
-    per-layer choice, and the generic decode kernel (QLDPC_NO_LAYERED_FAST).
+    every lanes-per-check width G (option ms_lanes_per_check), the default
+    per-layer choice, and the generic decode kernel (option layered_generic).
     Lane mappings never change the arithmetic."""
     from oracle import oracle
     from qldpcsim_amd import _lib, codes, schedule
     Hx, Hz = codes.load_code(code)
     if kernel == "generic":
-        monkeypatch.setenv("QLDPC_NO_LAYERED_FAST", "1")
+        qopt(layered_generic=1)
     elif kernel.startswith("G"):
-        monkeypatch.setenv("QLDPC_MS_LANES_PER_CHECK", kernel[1:])
+        qopt(ms_lanes_per_check=int(kernel[1:]))
     lx, _ = schedule.select_layers(Hx, Hz, "L")
     lp, lr = schedule.pack_layers(lx, Hz.shape[0])
     rng = np.random.default_rng(11)
@@ -336,16 +336,15 @@ def test_ms_layered_irregular_columns_match_oracle(dec, sched):
 @pytest.mark.parametrize("code,w,lg", [("LP118_2", "4", "1"), ("LP04_0", "8", "1"), ("LP118_0", "4", "1"),
                                         ("LP118_2", "4", "0"), ("LP118_2", "8", "0"), ("LP04_0", "4", "0"),
                                         ("LP118_0", "8", "0")])
-def test_bp_team_layered_kernels_match_oracle(dec, code, w, lg, monkeypatch):
+def test_bp_team_layered_kernels_match_oracle(dec, code, w, lg, qopt):
     """Layered BP teams: bp_team_lg_kernel (every graph table in global
     memory, the default) and the all-LDS bp_team_kernel<true, ..> (the
     fallback for schedules without the global image, forced by
-    QLDPC_BP_LG=0) at both team widths: bit-exact vs the oracle on channel and
+    option bp_lg = 0) at both team widths: bit-exact vs the oracle on channel and
     fixed-work syndromes."""
     from oracle import oracle
     from qldpcsim_amd import _lib, codes, schedule
-    monkeypatch.setenv("QLDPC_BP_LG", lg)
-    monkeypatch.setenv("QLDPC_BP_TEAM_W", w)
+    qopt(bp_lg=int(lg), bp_team_w=int(w))
     Hx, Hz = codes.load_code(code)
     lx, _ = schedule.select_layers(Hx, Hz, "L")
     lp, lr = schedule.pack_layers(lx, Hz.shape[0])

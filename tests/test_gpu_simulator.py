@@ -272,7 +272,7 @@ def _oracle_counters(Hx, Hz, sched, decType, osd, p, max_iter, sy_z, sy_x, errX,
     ("BP", 4, 0.05, 100, 330, 100),    # configs[4]: LP118_2 BP layered (OSDorder ignored, :281-282)
 ])
 def test_device_pipeline_counters_exact_on_configs_workload(decType, osd, p, max_iter, shots, batch, device_min,
-                                                            monkeypatch):
+                                                            osdpol):
     """The device simulate_p path (Philox sampler -> decode -> pinned
     posterior staging -> host reliability order -> GPU OSD -> on-device
     counters, two batch slots in flight) over 4 pipelined batches gives
@@ -280,7 +280,7 @@ def test_device_pipeline_counters_exact_on_configs_workload(decType, osd, p, max
     with the same shots."""
     import torch
     from qldpcsim_amd import codes, simulator
-    monkeypatch.setenv("QLDPC_OSD_DEVICE_MIN", device_min)
+    osdpol(device_min=int(device_min))
     Hx, Hz = codes.load_code("LP118_2")
     seed = 11
     got = simulator.simulate_p(Hx, Hz, p, shots=shots, decType=decType, decIterations=max_iter,

@@ -52,3 +52,26 @@ def test_op_equals_decode_batch(code, sched, algo):
     eb, itb, _, _ = torch.ops.qldpc.decode(decoders.pack_bits(syn), H, lp, lr, 0.02, 20, algo, 0.75, 1e-9,
                                           False, True)
     assert torch.equal(decoders.unpack_bits(eb, Hz.shape[1]), ref.ehat) and torch.equal(itb, ref.iters)
+
+
+@pytest.mark.gpu
+def test_op_cache_hits_by_content_and_release():
+    """The op's graph cache is keyed by H's content (a copy of H hits it, an
+    edited H does not) and torch.ops.qldpc.release() frees it; decoding after
+    a release rebuilds the graph and gives the same results."""
+    from qldpcsim_amd import decoders
+    Hz, H, lp, lr = _args("LP04_0", "F")
+    g = torch.Generator(device="cuda").manual_seed(4)
+    syn = torch.randint(0, 2, (300, Hz.shape[0]), dtype=torch.uint8, device="cuda", generator=g)
+    a = torch.ops.qldpc.decode(syn, H, lp, lr, 0.03, 15, "MS", 0.75, 1e-9, True, False)
+    b = torch.ops.qldpc.decode(syn, H.clone(), lp, lr, 0.03, 15, "MS", 0.75, 1e-9, True, False)
+    assert all(torch.equal(x, y) for x, y in zip(a, b))
+    H2 = H.clone()
+    H2[0, :] = 0                                            # a different matrix: its own graph
+    c = torch.ops.qldpc.decode(syn, H2, lp, lr, 0.03, 15, "MS", 0.75, 1e-9, True, False)
+    ref2 = decoders.decode_batch(H2.numpy(), syn, 0.03, 15, algo="MS", layer_ptr=lp.numpy(),
+                                 layer_rows=lr.numpy(), want_post=True)
+    assert torch.equal(c[0], ref2.ehat) and torch.equal(c[1], ref2.iters)
+    torch.ops.qldpc.release()
+    d = torch.ops.qldpc.decode(syn, H, lp, lr, 0.03, 15, "MS", 0.75, 1e-9, True, False)
+    assert all(torch.equal(x, y) for x, y in zip(a, d))

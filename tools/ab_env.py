@@ -1,6 +1,8 @@
-"""Interleaved A/B of an environment switch on one config (same box, same process per run).
-usage: python tools/ab_env.py ENVVAR[=VALUE] code algo sched p max_iter batch [rounds]
-("on" sets ENVVAR to VALUE, default 1; ENVVAR=ON/OFF sets OFF for "off" instead of unsetting)"""
+"""Interleaved A/B of a switch on one config (same box, one process per run).
+usage: python tools/ab_env.py SWITCH[=VALUE] code algo sched p max_iter batch [rounds]
+SWITCH is an environment variable, or a lower-case library option (include/
+qldpc_decoder.h, qldpc_set_option), passed as QLDPC_OPTIONS=name=value.
+("on" sets it to VALUE, default 1; SWITCH=ON/OFF sets OFF for "off" instead of unsetting)"""
 import json
 import os
 import subprocess
@@ -18,10 +20,12 @@ res = {"off": [], "on": []}
 for r in range(rounds):
     for k in (("off", "on") if r % 2 == 0 else ("on", "off")):
         env = dict(os.environ)
-        if k == "on":
-            env[env_var] = env_val or "1"
-        elif env_off:
-            env[env_var] = env_off
+        val = (env_val or "1") if k == "on" else env_off
+        if env_var.islower():                                  # a library option
+            if val:
+                env["QLDPC_OPTIONS"] = f"{env_var}={val}"
+        elif val:
+            env[env_var] = val
         else:
             env.pop(env_var, None)
         out = subprocess.run([sys.executable, "-c", snippet], env=env, capture_output=True, text=True)

@@ -64,11 +64,11 @@ def run(code, algo, sched, p, max_iter, B, reps=2):
 
 def run_hbm(n, dv, dc, algo, p, max_iter, B, force_code=None):
     """The HBM-resident kernel: a synthetic (dv, dc)-regular code of n
-    variables (or a bundled code with QLDPC_FORCE_HBM), one launch per half;
+    variables (or a bundled code with the force_hbm option), one launch per half;
     achieved GB/s under SURVEY.md 8(d)'s streaming model, w(3E + 2n) bytes
     per executed half-shot iteration (w = 4 MS / 8 BP), against 8 TB/s."""
     if force_code:
-        os.environ["QLDPC_FORCE_HBM"] = "1"
+        _lib.set_option("force_hbm", 1)
         Hx, Hz = codes.load_code(force_code)
         H = Hz
     else:
@@ -96,7 +96,7 @@ def run_hbm(n, dv, dc, algo, p, max_iter, B, force_code=None):
     its = int(r.iters.sum().item())
     ms, nl = _lib.timing_read()
     _lib.timing_enable(False)
-    os.environ.pop("QLDPC_FORCE_HBM", None)
+    _lib.set_option("force_hbm", 0)
     w = 4 if algo == "MS" else 8
     byts = its * (w * (3 * E + 2 * n)) + B * (m + n + 4)
     return {"hbm_kernel": name, "code": force_code or f"regular({dv},{dc}) n={n}", "m": m, "n": n, "E": E,

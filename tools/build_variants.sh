@@ -8,13 +8,12 @@ while [ $# -ge 2 ]; do
   if [ "$flags" = "HEAD" ]; then
     tmp=$(mktemp -d)
     (cd "$ROOT" && git archive HEAD qldpcsim_amd/csrc include) | tar -x -C "$tmp"
-    cp "$ROOT/qldpcsim_amd/csrc/Makefile" "$tmp/qldpcsim_amd/csrc/Makefile"
     rm -f "$ROOT/qldpcsim_amd/_build/var_$name.so"   # archived sources carry old mtimes: make would skip
     make -s -C "$tmp/qldpcsim_amd/csrc" OUT_DIR="$ROOT/qldpcsim_amd/_build" LIB=var_$name.so 2>&1 | grep -i error || true
     rm -rf "$tmp"
   else
     touch "$ROOT/qldpcsim_amd/csrc/decoder_kernels.hip"
-    make -s -C "$ROOT/qldpcsim_amd/csrc" LIB=var_$name.so EXTRA="$flags" 2>&1 | grep -i error || true
+    make -s -C "$ROOT/qldpcsim_amd/csrc" LIB=var_$name.so EXTRA="-DQLDPC_EXPERIMENTS $flags" 2>&1 | grep -i error || true
   fi
   ls -la "$ROOT/qldpcsim_amd/_build/var_$name.so"
 done

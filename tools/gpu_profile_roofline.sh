@@ -11,7 +11,8 @@ PASSES=("FETCH_SIZE"
         "WRITE_SIZE"
         "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"
         "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_FMA_F32"
-        "SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU")
+        "SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU"
+        "SQ_INSTS_LDS_STORE SQ_INSTS_LDS_LOAD SQ_INSTS_LDS_STORE_BANDWIDTH SQ_INSTS_LDS_LOAD_BANDWIDTH SQ_INSTS_LDS")
 while [ $# -ge 2 ]; do
   NAME=$1; ARGS=$2; shift 2
   D=gpurun_out/roof_$TAG/$NAME

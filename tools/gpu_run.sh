@@ -12,6 +12,7 @@
 #   sim3 / sim4    tools/bench_sim.py p-sweep of configs[3] / configs[4]
 #   cfg3prof       per-kernel counters of one configs[3] p = 0.1 batch (tools/gpu_profile_program.sh)
 #   osd            tools/osd_bench.py on the configs[3] p = 0.1 OSD shots
+#   osdab:LIBS     interleaved A/B of the device OSD (tools/osd_bench.py, configs[3] p = 0.1) over library builds
 #   ab:LIBS:CFGS   interleaved A/B (tools/ab_libs.py) of qldpcsim_amd/_build/var_<name>.so builds;
 #                  LIBS = comma-separated names (main = the in-tree build), CFGS = cfg preset names
 #                  (flood, msl2p05, msl2p10, msl0, bpl2p10, bpl2p05, bpf0, hbm) joined by commas
@@ -85,6 +86,22 @@ for l in open('$L'):
       L=$O/${TAG}_osd.log
       timeout -k 10 300 python -u tools/osd_bench.py LP118_2 MS L 50 0.1 131072 0 5 > $L 2>&1 || fail $step $? $L
       tail -4 $L ;;
+    osdab:*)
+      IFS=: read -r _ libs <<< "$step"
+      L=$O/${TAG}_osdab_${libs//,/_}.jsonl
+      : > $L
+      for r in 1 2 3; do
+        for l in ${libs//,/ }; do
+          [ $l = main ] && P=$B/libqldpc_hip.so || P=$B/var_$l.so
+          QLDPC_LIB=$P timeout -k 10 200 python -u tools/osd_bench.py LP118_2 MS L 50 0.1 131072 0 5 >> $L 2>> $O/${TAG}_osdab.err || fail $step $? $O/${TAG}_osdab.err
+        done
+      done
+      python3 -c "
+import json,collections
+d=collections.defaultdict(list); sh=collections.defaultdict(set)
+for l in open('$L'):
+    x=json.loads(l); d[x['lib']].append(round(x['sec']*1e3,2)); sh[x['lib']].add((x['ehat_sha'], str(x['status_hist'])))
+for k in d: print(k, sorted(d[k]), sh[k])" ;;
     ab:*)
       IFS=: read -r _ libs cfgs <<< "$step"
       A=()

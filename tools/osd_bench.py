@@ -47,7 +47,10 @@ for rep in range(reps + 1):
     if rep:
         times.append(time.perf_counter() - t)
 hist = np.bincount(status.cpu().numpy(), minlength=4).tolist()
+import hashlib  # noqa: E402
+ehat_sha = hashlib.sha256(e.cpu().numpy().tobytes() + status.cpu().numpy().tobytes()).hexdigest()[:16]
 t = float(np.median(times))
 print(json.dumps({"code": code, "dec": dec, "sched": sched, "p": p, "B": B, "order": order,
-                  "osd_shots": k, "sec": t, "osd_shots_per_s": k / t, "status_hist": hist,
+                  "osd_shots": k, "sec": t, "osd_shots_per_s": k / t, "status_hist": hist, "ehat_sha": ehat_sha,
+                  "lib": os.path.basename(_lib.LIB_PATH),
                   "kernel": os.environ.get("QLDPC_OSD_KERNEL", "block")}))
