@@ -187,9 +187,11 @@ def test_forced_hbm_non_partition_schedule(algo, qopt):
 
 
 @pytest.mark.parametrize("algo,sched", [("MS", "F"), ("MS", "L"), ("BP", "F"), ("BP", "L")])
-def test_rows_wider_than_64_edges_decode(algo, sched):
+def test_rows_wider_than_64_edges_decode(algo, sched, qopt):
     """Row degree 100 (the reference's decoders take any H): the HBM kernel's
-    two-pass check node for rows past its 64-edge registers, against the
+    two-pass check node for rows past its 64-edge registers (the default for
+    MS, whose LDS kernels take rows up to 32 edges; forced for BP, whose
+    generic LDS kernel takes any row degree and is checked too), against the
     oracle bit for bit on converging and fixed-work syndromes, 80 half-shots
     (64-slot tiles recycled)."""
     from qldpcsim_amd import _lib, schedule
@@ -197,7 +199,10 @@ def test_rows_wider_than_64_edges_decode(algo, sched):
     assert H.sum(axis=1).max() > 64
     layers = [np.arange(H.shape[0])] if sched == "F" else schedule.layerize(H)
     lp, lr = schedule.pack_layers(layers, H.shape[0])
-    assert _lib.kernel_name(H, lp, lr, algo) == f"hbm_tile_kernel<{0 if algo == 'MS' else 1}, 64, 4>"
     syn = np.concatenate([_syndromes(H, 60, 0.004, 3), np.random.default_rng(4).integers(0, 2, (20, H.shape[0]),
                                                                                          dtype=np.uint8)])
-    _check(H, syn, algo, 0.004, 8 if algo == "BP" else 15, lp, lr)
+    it = 8 if algo == "BP" else 15
+    _check(H, syn, algo, 0.004, it, lp, lr)                 # the default kernel
+    qopt(force_hbm=1)
+    assert _lib.kernel_name(H, lp, lr, algo) == f"hbm_tile_kernel<{0 if algo == 'MS' else 1}, 64, 4>"
+    _check(H, syn, algo, 0.004, it, lp, lr)

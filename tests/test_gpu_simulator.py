@@ -311,3 +311,54 @@ def test_simulator_refuses_more_ranks_than_gpus_over_rccl(monkeypatch):
     monkeypatch.delenv("QLDPC_SIM_BACKEND", raising=False)
     with pytest.raises(RuntimeError, match="HIP device"):
         simulator._init_dist_from_env()
+
+
+@pytest.mark.parametrize("device_min", ["1", "4096"])   # device reliability order / host order
+def test_two_ranks_configs3_pipeline_counters_exact(tmp_path, device_min):
+    """configs[3]'s pipeline (LP118_2 MS layered + OSD-0, p = 0.1, 50
+    iterations) under `torchrun --nproc-per-node 2` (gloo, both ranks on the
+    one GPU, 2 batches each): the all-reduced counters equal EXACTLY the sum
+    of the reference's per-shot loop run on the oracle over each rank's own
+    shots — rank r's contiguous share, drawn from its Philox key (rngSeed, r)
+    — i.e. the sharding adds, drops and repeats no shot (simulator.py:244-315)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    import torch
+    from conftest import ROOT
+    from qldpcsim_amd import codes, simulator
+    Hx, Hz = codes.load_code("LP118_2")
+    np.save(tmp_path / "Hx.npy", Hx.astype(np.int64))
+    np.save(tmp_path / "Hz.npy", Hz.astype(np.int64))
+    res = tmp_path / "res.json"
+    shots, seed, p, it = 241, 13, 0.1, 50
+    env = dict(os.environ, QLDPC_SIM_BACKEND="gloo", QLDPC_OSD_DEVICE_MIN=device_min)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29537", "-m", "qldpcsim_amd.simulator",
+                        "--Hx", str(tmp_path / "Hx.npy"), "--Hz", str(tmp_path / "Hz.npy"), "--p", str(p),
+                        "--shots", str(shots), "--decIterations", str(it), "--decSchedule", "L",
+                        "--OSDorder", "0", "--rngSeed", str(seed), "--batch", "64", "--results", str(res)],
+                       cwd=ROOT, capture_output=True, text=True, timeout=110, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = json.loads(res.read_text())["results"][str(p)]
+    want = {k: 0 for k in ("DecFailures_X", "DecFailures_Z", "decSuccessExact", "decSuccessDegen")}
+    its = [0.0, 0.0]
+    capped = 0
+    for rank in range(2):
+        my = shots // 2 + (1 if rank < shots % 2 else 0)
+        key = np.random.SeedSequence([seed, rank]).generate_state(1, np.uint64)[0]
+        ch = simulator.DeviceChannel(Hx, Hz, torch.device("cuda", 0), key)
+        sy_z, sy_x, ewX, ewZ = ch.sample(p, my)
+        w, c = _oracle_counters(Hx, Hz, "L", "MS", 0, p, it, sy_z.cpu().numpy(), sy_x.cpu().numpy(),
+                                ch.unpack(ewX).cpu().numpy(), ch.unpack(ewZ).cpu().numpy())
+        for k in want:
+            want[k] += w[k]
+        its[0] += w["Avg_number_of_iterations_X"] * my
+        its[1] += w["Avg_number_of_iterations_Z"] * my
+        capped += c
+    for k in want:
+        assert got[k] == want[k], (k, got[k], want[k])
+    assert abs(got["Avg_number_of_iterations_X"] - its[0] / shots) < 1e-9
+    assert abs(got["Avg_number_of_iterations_Z"] - its[1] / shots) < 1e-9
+    assert capped > 50                                      # OSD ran on many shots of both ranks
