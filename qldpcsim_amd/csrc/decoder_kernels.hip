@@ -1583,9 +1583,10 @@ __device__ __forceinline__ uint32_t cn_bp_word(const DecodeArgs& a, const qldpc_
       th2 = P / th;
     else
       th2 = QLDPC_DIV(P, th);
-    // (:257-258): |th2| >= 1 - eps implies th2 != 0, so eps * sign(th2) is
-    // copysign(eps, th2) (a NaN compares false and stays)
-    th2 = (__builtin_fabs(th2) >= 1.0 - a.eps) ? th2 - __builtin_copysign(a.eps, th2) : th2;
+    // (:257-258): |th2| >= 1 - eps implies th2 != 0, so th2 - eps sign(th2)
+    // is copysign(|th2| - eps, th2) (round-to-nearest is symmetric in sign;
+    // a NaN compares false and stays)
+    th2 = (__builtin_fabs(th2) >= 1.0 - a.eps) ? __builtin_copysign(__builtin_fabs(th2) - a.eps, th2) : th2;
     double val = 2.0 * qldpc_atanh_t(th2, lt->atanh_hl, lt->atanh_rcp);   // (:259) np.arctanh
     if (synb) val = -val;                                 // (:260-261)
     if (!__builtin_isfinite(val)) fl |= FLAG_NONFINITE;

@@ -7,9 +7,11 @@
 #   bench          bench.py --steps 20 --warmup 5 (headline)  -> gpurun_out/TAG_bench.log
 #   bench-cfg      bench.py on the configs[2]-[4] decoders    -> gpurun_out/TAG_bench_cfg.jsonl
 #   roof-decoders  counter profile (tools/gpu_profile_roofline.sh) of the configs[2]-[4] decoders
+#   roof-bp / roof-msl  counter profiles of the BP decoders / the layered MS decoder only
 #   roof-flood     counter profile of the headline kernel
 #   roof-hbm       counter profile of the HBM-resident kernel on the headline workload
 #   sim3 / sim4    tools/bench_sim.py p-sweep of configs[3] / configs[4]
+#   phases3        tools/prof_sim.py phase times of one configs[3] p = 0.1 batch
 #   cfg3prof       per-kernel counters of one configs[3] p = 0.1 batch (tools/gpu_profile_program.sh)
 #   osd            tools/osd_bench.py on the configs[3] p = 0.1 OSD shots
 #   osdab:LIBS     interleaved A/B of the device OSD (tools/osd_bench.py, configs[3] p = 0.1) over library builds
@@ -71,6 +73,10 @@ for l in open('$L'):
     roof-decoders)
       bash tools/gpu_profile_roofline.sh $TAG msl2p05 "${CFG[msl2p05]}" msl2p10 "${CFG[msl2p10]}" \
         bpl2p10 "${CFG[bpl2p10]}" bpf0 "${CFG[bpf0]}" || fail $step $? ;;
+    roof-bp)
+      bash tools/gpu_profile_roofline.sh ${TAG}b bpl2p10 "${CFG[bpl2p10]}" bpf0 "${CFG[bpf0]}" || fail $step $? ;;
+    roof-msl)
+      bash tools/gpu_profile_roofline.sh ${TAG}m msl2p05 "${CFG[msl2p05]}" msl2p10 "${CFG[msl2p10]}" || fail $step $? ;;
     roof-flood)
       bash tools/gpu_profile_roofline.sh ${TAG}f flood "" || fail $step $? ;;
     roof-hbm)
@@ -80,6 +86,9 @@ for l in open('$L'):
       [ $step = sim3 ] && W=LP118_2:MS || W=LP118_2:BP
       timeout -k 10 700 python -u tools/bench_sim.py 1048576 $W > $L 2>&1 || fail $step $? $L
       grep shots_per_s $L | cut -c1-160 ;;
+    phases3)
+      L=$O/${TAG}_phases3.json
+      timeout -k 10 300 python -u tools/prof_sim.py LP118_2 MS L 0 50 0.1 131072 > $L 2>&1 || fail $step $? $L ;;
     cfg3prof)
       bash tools/gpu_profile_program.sh ${TAG}_cfg3 tools/prof_sim.py LP118_2 MS L 0 50 0.1 131072 || fail $step $? ;;
     osd)
