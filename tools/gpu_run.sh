@@ -16,7 +16,8 @@
 #   osd            tools/osd_bench.py on the configs[3] p = 0.1 OSD shots
 #   osdab:LIBS     interleaved A/B of the device OSD (tools/osd_bench.py, configs[3] p = 0.1) over library builds
 #   ab:LIBS:CFGS   interleaved A/B (tools/ab_libs.py) of qldpcsim_amd/_build/var_<name>.so builds;
-#                  LIBS = comma-separated names (main = the in-tree build), CFGS = cfg preset names
+#                  LIBS = comma-separated names (main = the in-tree build; name+opt=v+opt=v adds
+#                  library options), CFGS = cfg preset names
 #                  (flood, msl2p05, msl2p10, msl0, bpl2p10, bpl2p05, bpf0, hbm) joined by commas
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -114,7 +115,11 @@ for k in d: print(k, sorted(d[k]), sh[k])" ;;
     ab:*)
       IFS=: read -r _ libs cfgs <<< "$step"
       A=()
-      for l in ${libs//,/ }; do [ $l = main ] && A+=($B/libqldpc_hip.so) || A+=($B/var_$l.so); done
+      for l in ${libs//,/ }; do
+        # name+opt=v+opt=v: library options for that entry (QLDPC_OPTIONS)
+        n=${l%%+*}; o=; [ "$n" != "$l" ] && o=@${l#*+} && o=${o//+/,}
+        [ $n = main ] && A+=($B/libqldpc_hip.so$o) || A+=($B/var_$n.so$o)
+      done
       C=()
       for c in ${cfgs//,/ }; do C+=(--cfg "${CFG[$c]}"); done
       L=$O/${TAG}_ab_${libs//,/_}.json
