@@ -227,6 +227,18 @@ def algorithmic_bytes_per_iter(H, layer_ptr, layer_rows, word):
     return tot
 
 
+def structural_bytes_per_iter(H, layer_ptr, layer_rows, word):
+    """What hbm_tile_kernel itself moves per executed half-shot iteration:
+    the §8(d) model plus one column-sum read per edge (the exact check node
+    needs S_j and c2v_e on every edge): flooding w(4E + 2n)."""
+    m, _ = H.shape
+    if len(layer_ptr) == 2 and layer_ptr[1] == m:
+        e_sched = int(H.sum())
+    else:
+        e_sched = sum(int(H[layer_rows[layer_ptr[l]:layer_ptr[l + 1]]].sum()) for l in range(len(layer_ptr) - 1))
+    return algorithmic_bytes_per_iter(H, layer_ptr, layer_rows, word) + word * e_sched
+
+
 # ---------------------------------------------------------------------------
 # CPU baselines (rank 0, N = 1): bounded samples of the same workload
 # ---------------------------------------------------------------------------
@@ -512,6 +524,9 @@ def hbm_streaming_leg(halves, outs, prior, args, B, bits, algo_launch, dev, step
         _lib.timing_enable(False)
     t_launch = kern_ms / 1e3 / launches
     gbs = algo_launch / t_launch / 1e9
+    H0, _, lp0, lr0 = halves[0]
+    w = 8 if args.algo == "BP" else 4
+    struct = structural_bytes_per_iter(H0, lp0, lr0, w) / algorithmic_bytes_per_iter(H0, lp0, lr0, w)
     measured = None
     _, prof = find_profile(name, None, kernel_code_sha(_lib.LIB_PATH, name))
     if prof is not None:                               # PMC bytes per half-shot of this kernel build
@@ -520,10 +535,11 @@ def hbm_streaming_leg(halves, outs, prior, args, B, bits, algo_launch, dev, step
             "measured_gbs": measured, "measured_frac": None if measured is None else measured / HBM_PEAK_GBS,
             "kernel_ms_per_launch": t_launch * 1e3, "algorithmic_gbs": gbs, "peak_gbs": HBM_PEAK_GBS,
             "frac": gbs / HBM_PEAK_GBS,
+            "structural_over_model": struct, "structural_gbs": gbs * struct,
             "note": "the same workload and iteration counts through the HBM-resident decoder "
-                    "(option force_hbm); GB/s under SURVEY.md 8d's algorithmic model (the kernel moves "
-                    "about 1.27x those bytes: post and c2v rows both read per edge); the headline value is "
-                    "the LDS-resident kernel's"}
+                    "(option force_hbm); GB/s under SURVEY.md 8d's algorithmic model; the kernel's "
+                    "structural bytes (structural_gbs) add one column-sum read per edge, the floor of an "
+                    "exact check node (DESIGN.md 3.6); the headline value is the LDS-resident kernel's"}
 
 
 def roofline(names, t_launch, hs_launch, it_launch, algo_launch, launches):
