@@ -119,8 +119,10 @@ typedef struct __attribute__((aligned(16))) {   /* 16-byte pair reads on the dev
 
 #define QLDPC_LIBM_TAB_INIT { QLDPC_TANH_LUT_INIT, QLDPC_ATANH_HL_INIT, QLDPC_ATANH_RCP_INIT }
 
-/* np.tanh (NumPy simd_tanh_f64). tc = qldpc_libm_tab.tanh_c. */
-QLDPC_HD double qldpc_tanh_t(double x, const double* tc) {
+/* np.tanh (NumPy simd_tanh_f64). tc = qldpc_libm_tab.tanh_c. fin != 0 (a
+   constant): the caller guarantees |x| < 2^1023 (no NaN, no infinity), where
+   the two range selects at the end are the identity, so they are left out. */
+QLDPC_HD double qldpc_tanh_x(double x, const double* tc, int fin) {
   const uint64_t u = qldpc_d2bits(x);
   const uint64_t nd = u & 0x7ff8000000000000ull;      /* exponent + top 3 mantissa bits */
   int32_t h = (int32_t)(uint32_t)(nd >> 32) - 0x3fc00000;
@@ -161,10 +163,12 @@ QLDPC_HD double qldpc_tanh_t(double x, const double* tc) {
   r = QLDPC_FMA(r, y, QLDPC_TC(2));
   r = QLDPC_FMA(r, y, QLDPC_TC(1));
 #undef QLDPC_TC
-  r = nd <= 0x7fe0000000000000ull ? r : 1.0;         /* |x| >= 2^1023, inf */
+  if (!fin) r = nd <= 0x7fe0000000000000ull ? r : 1.0;   /* |x| >= 2^1023, inf */
   r = qldpc_bits2d(qldpc_d2bits(r) | (u & 0x8000000000000000ull));
-  return (x == x) ? r : qldpc_bits2d(0x7ff8000000000000ull);
+  return (fin || x == x) ? r : qldpc_bits2d(0x7ff8000000000000ull);
 }
+
+QLDPC_HD double qldpc_tanh_t(double x, const double* tc) { return qldpc_tanh_x(x, tc, 0); }
 
 /* vrcp14pd(Y) rounded half-up to a 4-bit mantissa (SVML atanh), for a
    positive normal Y: R = 2^-e (1 - c/32) with c = the number of probed steps
@@ -182,13 +186,15 @@ QLDPC_HD double qldpc_svml_rrcp(double Y, const uint32_t* rb, double* ge, int* t
 
 /* np.arctanh (SVML __svml_atanh8_ha). hl = qldpc_libm_tab.atanh_hl, rb =
    .atanh_rcp. |x| >= 1 and NaN take SVML's rare path: +-inf at |x| == 1,
-   NaN otherwise (signs / payloads as below; BP flags them non-finite). */
-QLDPC_HD double qldpc_atanh_t(double x, const double* hl, const uint32_t* rb) {
+   NaN otherwise (signs / payloads as below; BP flags them non-finite).
+   fin != 0 (a constant): the caller guarantees |x| < 1, so the rare-path
+   tests are left out. */
+QLDPC_HD double qldpc_atanh_x(double x, const double* hl, const uint32_t* rb, int fin) {
   const uint64_t u = qldpc_d2bits(x);
   const uint64_t sgn = u & 0x8000000000000000ull;
   const double ax = qldpc_bits2d(u & 0x7fffffffffffffffull);
-  if (!(ax == ax)) return x;
-  if (ax >= 1.0) return qldpc_bits2d(((ax == 1.0) ? 0x7ff0000000000000ull : 0x7ff8000000000000ull) | sgn);
+  if (!fin && !(ax == ax)) return x;
+  if (!fin && ax >= 1.0) return qldpc_bits2d(((ax == 1.0) ? 0x7ff0000000000000ull : 0x7ff8000000000000ull) | sgn);
   const double Yp = ax + 1.0, Ym = 1.0 - ax;
   const double Yp_lo = ax - (Yp - 1.0);                /* 1 + ax = Yp + Yp_lo */
   const double Ym_nlo = ax + (Ym - 1.0);               /* 1 - ax = Ym - Ym_nlo */
@@ -237,6 +243,10 @@ QLDPC_HD double qldpc_atanh_t(double x, const double* hl, const uint32_t* rb) {
   const double e2 = dm + t5;                           /* (minus) rounding error of S2 */
   const double r = S2 + ((A + B) - e2);
   return r * qldpc_bits2d(0x3fe0000000000000ull | sgn);   /* +-0.5 */
+}
+
+QLDPC_HD double qldpc_atanh_t(double x, const double* hl, const uint32_t* rb) {
+  return qldpc_atanh_x(x, hl, rb, 0);
 }
 
 /* host image of the tables (the oracle, the library's host code; in HIP

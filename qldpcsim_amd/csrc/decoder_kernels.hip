@@ -1556,10 +1556,21 @@ __device__ __forceinline__ uint32_t cn_bp_word(const DecodeArgs& a, const qldpc_
                                                int k, int lane, uint32_t synb, const double* post, double* c2v,
                                                int& fl) {
   const bool ek = valid && k < DC;
+  // a wave with no check of this pass skips it (uniform); inside, every lane
+  // loads and computes (t = 0 for a pad edge / check: variable 0, position
+  // 0, in bounds) and the pad lanes' values are replaced by selects — no
+  // exec-masked branches around the loads and the tanh
+  if (ballot(valid) == 0) return 0u;
   const int j = (int)((t & 0xffffu) >> 3), p = (int)(t >> 18);
-  const double pj = ek ? post[j] : 0.0;
-  double th = 1.0;
-  if (ek) th = qldpc_tanh_t((pj - c2v[p]) / 2.0, lt->tanh_c);   // v2c (:269), np.tanh (:254)
+  const double pjr = post[j];
+  const double x = (pjr - c2v[p]) / 2.0;                      // v2c (:269)
+  double th;                                                  // np.tanh (:254)
+  if (__builtin_expect(ballot(!(__builtin_fabs(x) < 0x1p1023)) != 0, 0))
+    th = qldpc_tanh_x(x, lt->tanh_c, 0);                      // a NaN / huge argument in the wave
+  else
+    th = qldpc_tanh_x(x, lt->tanh_c, 1);
+  th = ek ? th : 1.0;
+  const double pj = ek ? pjr : 0.0;
   // np.prod: sequential left fold over the check's edges in ascending variable
   // order, ((t_0 t_1) t_2) ..., formed redundantly by every lane of the group
   // from the group's t values (one permute each): same rounding as a
@@ -1572,26 +1583,32 @@ __device__ __forceinline__ uint32_t cn_bp_word(const DecodeArgs& a, const qldpc_
   // parity of the hard decisions of the posteriors this check read (:283-285)
   const uint64_t hb = ballot(ek && pj < 0.0);
   const uint32_t par = (uint32_t)__builtin_popcount((uint32_t)(hb >> (lane & 56)) & 0xffu) & 1u;
-  if (ek) {
-    if (th == 0.0) fl |= FLAG_NONFINITE;
-    // P / th (:256). QLDPC_DIV is IEEE division for nonzero operands in the
-    // normal range (|th| <= 1 and |P| <= |th| here); a wave holding a zero
-    // (a -0 product keeps its sign only through v_div_fixup), tiny or
-    // non-finite one divides the general way.
-    double th2;
-    if (__builtin_expect(ballot(!(__builtin_fabs(th) > 1e-150 && __builtin_fabs(P) > 1e-150)) != 0, 0))
-      th2 = P / th;
-    else
-      th2 = QLDPC_DIV(P, th);
-    // (:257-258): |th2| >= 1 - eps implies th2 != 0, so th2 - eps sign(th2)
-    // is copysign(|th2| - eps, th2) (round-to-nearest is symmetric in sign;
-    // a NaN compares false and stays)
-    th2 = (__builtin_fabs(th2) >= 1.0 - a.eps) ? __builtin_copysign(__builtin_fabs(th2) - a.eps, th2) : th2;
-    double val = 2.0 * qldpc_atanh_t(th2, lt->atanh_hl, lt->atanh_rcp);   // (:259) np.arctanh
-    if (synb) val = -val;                                 // (:260-261)
-    if (!__builtin_isfinite(val)) fl |= FLAG_NONFINITE;
-    c2v[p] = val;
-  }
+  // Every lane computes (a pad lane: th = 1, its results discarded); only
+  // the message store is guarded.
+  // P / th (:256). QLDPC_DIV is IEEE division for nonzero operands in the
+  // normal range (|th| <= 1 and |P| <= |th| here); a wave holding a zero
+  // (a -0 product keeps its sign only through v_div_fixup), tiny or
+  // non-finite one divides the general way.
+  double th2;
+  if (__builtin_expect(ballot(ek && !(__builtin_fabs(th) > 1e-150 && __builtin_fabs(P) > 1e-150)) != 0, 0))
+    th2 = P / th;
+  else
+    th2 = QLDPC_DIV(P, th);
+  // (:257-258): |th2| >= 1 - eps implies th2 != 0, so th2 - eps sign(th2)
+  // is copysign(|th2| - eps, th2) (round-to-nearest is symmetric in sign;
+  // a NaN compares false and stays)
+  th2 = (__builtin_fabs(th2) >= 1.0 - a.eps) ? __builtin_copysign(__builtin_fabs(th2) - a.eps, th2) : th2;
+  // np.arctanh (:259); SVML's rare path (|th2| >= 1, NaN) only when a lane
+  // of the wave needs it
+  double at;
+  if (__builtin_expect(ballot(ek && !(__builtin_fabs(th2) < 1.0)) != 0, 0))
+    at = qldpc_atanh_x(th2, lt->atanh_hl, lt->atanh_rcp, 0);
+  else
+    at = qldpc_atanh_x(th2, lt->atanh_hl, lt->atanh_rcp, 1);
+  double val = 2.0 * at;
+  if (synb) val = -val;                                   // (:260-261)
+  if (ek && (th == 0.0 || !__builtin_isfinite(val))) fl |= FLAG_NONFINITE;
+  if (ek) c2v[p] = val;
   return valid ? (par ^ synb) : 0u;
 }
 
@@ -1599,7 +1616,8 @@ template <int DC>
 __device__ __forceinline__ uint32_t cn_bp_group(const DecodeArgs& a, const LdsView& g, int c, bool valid,
                                                 int k, int lane, uint32_t synb, const double* post,
                                                 double* c2v, int& fl) {
-  const uint32_t t = (valid && k < DC) ? g.cn_tab[8 * c + k] : 0u;
+  const uint32_t tw = g.cn_tab[8 * c + k];                     // (c = 0 for a pad check)
+  const uint32_t t = (valid && k < DC) ? tw : 0u;
   return cn_bp_word<DC>(a, g.lt, t, valid, k, lane, synb, post, c2v, fl);
 }
 

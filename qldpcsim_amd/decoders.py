@@ -18,7 +18,7 @@ cannot certify get NumPy's own order (decoders.py:320-325) on the host and
 the device elimination again. `OSDdec` / `apply_osd` are the single-shot and
 host entry points (host C++ elimination).
 
-Deviations from the reference (documented in DESIGN.md §6):
+Deviations from the reference (documented in DESIGN.md §7):
   * layers=None means flooding (the reference raises AttributeError on
     `np.range`, decoders.py:144 / :221).
   * H entries are reduced mod 2 (as load_matrix does, simulator.py:35);

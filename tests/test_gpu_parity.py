@@ -366,3 +366,33 @@ def test_bp_team_layered_kernels_match_oracle(dec, code, w, lg, qopt):
     np.testing.assert_array_equal(r.iters, it)
     np.testing.assert_array_equal(r.ehat, e)
     np.testing.assert_array_equal(r.post.view(np.uint64), post.view(np.uint64))
+
+
+@pytest.mark.parametrize("sched", ["F", "L"])
+@pytest.mark.parametrize("case", ["L0", "eps0"])
+def test_bp_nonfinite_paths_match_oracle(dec, sched, case):
+    """BP's rare arithmetic against the oracle, through the team kernels'
+    wave-uniform slow paths: p = 0.5 (L = 0: every first v2c is 0, tanh 0,
+    P / t = 0 / 0 = NaN, atanh(NaN)) and eps = 0 at p = 1e-20 (L = 46: tanh
+    rounds to +-1, th2 = +-1 unclipped, atanh = +-inf, then inf - inf).
+    Posteriors compare NaN-aware (NaN payloads are the platform's); every
+    shot the oracle flags (tanh = 0) is flagged non-finite on the GPU."""
+    from oracle import oracle
+    from qldpcsim_amd import _lib, codes, schedule
+    Hx, Hz = codes.load_code("LP118_0")
+    lp = lr = None
+    if sched == "L":
+        lx, _ = schedule.select_layers(Hx, Hz, "L")
+        lp, lr = schedule.pack_layers(lx, Hz.shape[0])
+    rng = np.random.default_rng(5)
+    syn = np.concatenate([rng.integers(0, 2, (96, Hz.shape[0]), dtype=np.uint8),
+                          _channel(Hx, Hz, 0.05, 96, 3)[0]])
+    p, eps = (0.5, 1e-9) if case == "L0" else (1e-20, 0.0)
+    r = dec.decode_batch(Hz, syn, p, 12, algo="BP", eps=eps, want_post=True, layer_ptr=lp, layer_rows=lr)
+    e, it, post, fl = oracle.decode_batch("BP", Hz, syn, p, 12, lp, lr, eps=eps)
+    assert not np.isfinite(post).all()                 # the rare paths ran
+    np.testing.assert_array_equal(r.iters, it)
+    np.testing.assert_array_equal(r.ehat, e)
+    np.testing.assert_array_equal(r.post, post)        # NaN == NaN here
+    gpu_nf = (r.flags & _lib.FLAG_NONFINITE) != 0
+    assert gpu_nf[(fl & 2) != 0].all()
