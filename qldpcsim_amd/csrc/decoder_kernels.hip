@@ -88,6 +88,31 @@ __device__ __forceinline__ double np_pairwise_sum(const double* a, int n) {
   return 0.0 + res;
 }
 
+// np_pairwise_sum of a BP column (variable node, decoders.py:276): below 8
+// terms NumPy adds sequentially from -0.0, so with K >= n terms loaded at
+// once (the c2v region is padded by 8 entries) and the terms past n replaced
+// by -0.0 — x + -0.0 == x for every x, -0.0 included — the sum is the same
+// bit for bit, without a load-wait-add chain per term. K is wave-uniform:
+// the smallest of 3 / 5 / 7 covering every active lane's n (ballots); a wave
+// holding a column of 8 or more terms takes the general pairwise sum.
+template <int K>
+__device__ __forceinline__ double np_sum_lt8(const double* a, int n) {
+  double x[K];
+#pragma unroll
+  for (int t = 0; t < K; ++t) x[t] = a[t];
+  double res = -0.0;
+#pragma unroll
+  for (int t = 0; t < K; ++t) res += (t < n) ? x[t] : -0.0;
+  return 0.0 + res;
+}
+
+__device__ __forceinline__ double np_sum_col(const double* a, int n) {
+  if (__builtin_expect(ballot(n >= 8) != 0, 0)) return np_pairwise_sum(a, n);
+  if (ballot(n > 3) == 0) return np_sum_lt8<3>(a, n);
+  if (ballot(n > 5) == 0) return np_sum_lt8<5>(a, n);
+  return np_sum_lt8<7>(a, n);
+}
+
 // Set bit `c` of a per-wave bit-word array for every lane whose predicate is
 // true, for a chunk of 64 consecutive indices starting at c0 (all lanes call).
 __device__ __forceinline__ void store_bits64(uint32_t* words, int c0, int pred, int lane) {
@@ -748,8 +773,8 @@ __device__ __forceinline__ double vn_post(const DecodeArgs& a, const LdsView& g,
     return a.L + (double)s;
   } else {
     const double* c2v = (const double*)c2v_raw;
-    if (d == 0) return a.L;                          // L_post[j] = L0 (:277-278)
-    return a.L + np_pairwise_sum(c2v + p0, d);
+    const double t = np_sum_col(c2v + p0, d);
+    return d == 0 ? a.L : a.L + t;                   // L_post[j] = L0 (:277-278)
   }
 }
 
@@ -1937,7 +1962,8 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
         auto vn = [&](uint32_t info) {
           const int j = (int)(info >> 21), d = (int)((info >> 16) & 31u);
           const double old = post[j];
-          const double nw = d == 0 ? L : L + np_pairwise_sum(c2v + (info & 0xffffu), d);   // (:276-278)
+          const double sc = np_sum_col(c2v + (info & 0xffffu), d);
+          const double nw = d == 0 ? L : L + sc;            // (:276-278)
           post[j] = nw;
           if ((old < 0.0) != (nw < 0.0)) acc ^= a.avar[j];
         };
