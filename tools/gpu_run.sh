@@ -93,6 +93,9 @@ for l in open('$L'):
     phases4)
       L=$O/${TAG}_phases4.json
       timeout -k 10 300 python -u tools/prof_sim.py LP118_2 BP L 4 100 0.1 65536 > $L 2>&1 || fail $step $? $L ;;
+    phases4b)
+      L=$O/${TAG}_phases4b.json
+      timeout -k 10 300 python -u tools/prof_sim.py LP118_2 BP L 4 100 0.1 262144 > $L 2>&1 || fail $step $? $L ;;
     cfg3prof)
       bash tools/gpu_profile_program.sh ${TAG}_cfg3 tools/prof_sim.py LP118_2 MS L 0 50 0.1 131072 || fail $step $? ;;
     osd)
