@@ -15,6 +15,7 @@
 #   cfg3prof       per-kernel counters of one configs[3] p = 0.1 batch (tools/gpu_profile_program.sh)
 #   osd            tools/osd_bench.py on the configs[3] p = 0.1 OSD shots
 #   osdab:LIBS     interleaved A/B of the device OSD (tools/osd_bench.py, configs[3] p = 0.1) over library builds
+#   simab:LIBS     configs[3] sweep (tools/bench_sim.py) per library build, two interleaved rounds
 #   ab:LIBS:CFGS   interleaved A/B (tools/ab_libs.py) of qldpcsim_amd/_build/var_<name>.so builds;
 #                  LIBS = comma-separated names (main = the in-tree build; name+opt=v+opt=v adds
 #                  library options), CFGS = cfg preset names
@@ -118,6 +119,19 @@ d=collections.defaultdict(list); sh=collections.defaultdict(set)
 for l in open('$L'):
     x=json.loads(l); d[x['lib']].append(round(x['sec']*1e3,2)); sh[x['lib']].add((x['ehat_sha'], str(x['status_hist'])))
 for k in d: print(k, sorted(d[k]), sh[k])" ;;
+    simab:*)
+      # configs[3] sweep (tools/bench_sim.py) per library build, two rounds
+      IFS=: read -r _ libs <<< "$step"
+      L=$O/${TAG}_simab_${libs//,/_}.jsonl
+      : > $L
+      for r in 1 2; do
+        for l in ${libs//,/ }; do
+          [ $l = main ] && P=$B/libqldpc_hip.so || P=$B/var_$l.so
+          echo "{\"lib\": \"$l\", \"round\": $r}" >> $L
+          QLDPC_LIB=$P timeout -k 10 400 python -u tools/bench_sim.py 1048576 LP118_2:MS >> $L 2>> $O/${TAG}_simab.err || fail $step $? $O/${TAG}_simab.err
+        done
+      done
+      grep -o '"lib": "[a-z0-9]*"\|"p": [0-9.]*\|"shots_per_s": [0-9.]*' $L | paste -sd' ' | sed 's/"lib"/\n"lib"/g' ;;
     ab:*)
       IFS=: read -r _ libs cfgs <<< "$step"
       A=()
