@@ -452,6 +452,13 @@ def run_rank(args, rank, world, local):
     io_bytes = 8 * ((m + 63) // 64 + (n + 63) // 64) + 4 if bits else m + n + 4
     algo_launch = algo_bytes * it_per_launch + io_bytes * hs_per_launch
     roof = roofline(names, avg_launch_s, hs_per_launch, it_per_launch, algo_launch, launches)
+    try:                                   # launch geometry (older library builds lack the call)
+        H0, _, lp0, lr0 = halves[0]
+        w, b, lds = _lib.launch_info(H0, lp0, lr0, args.algo, dev.index)
+        roof["occupancy"] = {"waves_per_workgroup": w, "workgroups_per_cu": b, "waves_per_cu": w * b,
+                             "lds_bytes_per_workgroup": lds}
+    except (AttributeError, RuntimeError, ValueError):
+        pass
 
     hbm_leg = None
     if world == 1 and args.hbm_leg and not args.worklog and args.path != "hbm":

@@ -120,6 +120,12 @@ int qldpc_decode_device(const qldpc_code *code, const qldpc_schedule *sched, int
 int qldpc_decode_kernel_name(const qldpc_code *code, const qldpc_schedule *sched, int algo,
                              char *buf, int len);
 
+/* The launch geometry of that kernel: waves per workgroup, resident
+ * workgroups per CU and LDS bytes per workgroup (0, 0, 0 for the
+ * HBM-resident kernel, whose geometry is fixed). Measurement only. */
+int qldpc_decode_launch_info(const qldpc_code *code, const qldpc_schedule *sched, int algo,
+                             int *waves_per_wg, int *wg_per_cu, int *lds_bytes);
+
 /* qldpc_decode_device with a choice of formats: d_syn uint8 [batch][m]
  * (QLDPC_FMT_BYTES) or uint64 [batch][ceil(m/64)] (QLDPC_FMT_BITS); d_ehat
  * uint8 [batch][n] or uint64 [batch][ceil(n/64)]. Bit-packed I/O cuts the

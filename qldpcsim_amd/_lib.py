@@ -25,6 +25,7 @@ EXPORTS = (
     "qldpc_code_create", "qldpc_code_destroy", "qldpc_code_shape",
     "qldpc_schedule_create", "qldpc_schedule_destroy", "qldpc_schedule_release_workspace",
     "qldpc_decode_device", "qldpc_decode_device_ex", "qldpc_decode_host", "qldpc_decode_kernel_name",
+    "qldpc_decode_launch_info",
     "qldpc_osd_decode", "qldpc_osd_decode_batch", "qldpc_osd_device", "qldpc_osd_order_device",
     "qldpc_osd_device_ordered", "qldpc_osd_device_ordered_ex", "qldpc_cpython_setdiff_first",
     "qldpc_channel_thresholds", "qldpc_channel_sample", "qldpc_channel_sample_ex", "qldpc_count_outcomes",
@@ -69,6 +70,7 @@ def _load():
         "qldpc_decode_device_ex": ([P, P, I, P, I, I64, D, I, D, D, P, I, P, P, P, P], I),
         "qldpc_decode_host": ([P, P, I, P, I64, D, I, D, D, P, P, P, P], I),
         "qldpc_decode_kernel_name": ([P, P, I, ctypes.c_char_p, I], I),
+        "qldpc_decode_launch_info": ([P, P, I, ctypes.POINTER(I), ctypes.POINTER(I), ctypes.POINTER(I)], I),
         "qldpc_osd_decode": ([P, P, P, I, P, P, P, I], I),
         "qldpc_osd_decode_batch": ([P, I64, P, P, I, P, I], I),
         "qldpc_osd_device": ([P, I64, P, P, I, P, P, P], I),
@@ -231,6 +233,17 @@ def kernel_name(H, layer_ptr, layer_rows, algo, device_index=None):
     buf = ctypes.create_string_buffer(128)
     check(lib.qldpc_decode_kernel_name(code.handle, sched.handle, ALGO[algo], buf, 128))
     return buf.value.decode()
+
+
+def launch_info(H, layer_ptr, layer_rows, algo, device_index=None):
+    """(waves per workgroup, workgroups per CU, LDS bytes per workgroup) of
+    that kernel's launch; zeros for the HBM-resident kernel."""
+    code = code_for(H, device_index)
+    sched = code.schedule(layer_ptr, layer_rows)
+    w, b, l = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    check(lib.qldpc_decode_launch_info(code.handle, sched.handle, ALGO[algo], ctypes.byref(w), ctypes.byref(b),
+                                       ctypes.byref(l)))
+    return w.value, b.value, l.value
 
 
 def timing_enable(on=True):

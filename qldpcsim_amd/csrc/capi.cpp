@@ -1164,6 +1164,22 @@ extern "C" int qldpc_decode_kernel_name(const qldpc_code* code, const qldpc_sche
   return QLDPC_OK;
 }
 
+extern "C" int qldpc_decode_launch_info(const qldpc_code* code, const qldpc_schedule* sched_c, int algo,
+                                        int* waves_per_wg, int* wg_per_cu, int* lds_bytes) {
+  auto* sched = const_cast<qldpc_schedule*>(sched_c);
+  if (!code || !sched || !waves_per_wg || !wg_per_cu || !lds_bytes) return fail(QLDPC_EINVAL, "null argument");
+  if (algo != QLDPC_ALGO_MS && algo != QLDPC_ALGO_BP) return fail(QLDPC_EINVAL, "Unrecognized decoder type.");
+  if (code->device < 0 || !sched->d_blob) return fail(QLDPC_EHIP, "no HIP device was visible when the code/schedule was created");
+  LaunchCfg* cfg = nullptr;
+  bool hbm = false;
+  int rc = choose_path(sched, algo, &cfg, &hbm);
+  if (rc) return rc;
+  *waves_per_wg = hbm ? 0 : cfg->waves;
+  *wg_per_cu = hbm ? 0 : cfg->blocks_per_cu;
+  *lds_bytes = hbm ? 0 : cfg->lds;
+  return QLDPC_OK;
+}
+
 extern "C" int qldpc_decode_host(const qldpc_code* code_c, const qldpc_schedule* sched, int algo,
                                  const uint8_t* h_syn, int64_t batch, double p, int max_iter,
                                  double beta, double eps, uint8_t* h_ehat, int32_t* h_iters,
