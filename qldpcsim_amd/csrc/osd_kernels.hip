@@ -60,6 +60,37 @@ __device__ __forceinline__ void spill_shot(const OsdArgs& a, long long shot, int
   if (threadIdx.x == 0) a.spill_idx[q] = (int32_t)(a.shot_base + shot);
 }
 
+// Shots whose certification (below) cannot succeed, told apart before the
+// elimination: when the run of near-tied keys that ends the device order
+// starts inside the first rank(H) positions, the decision prefix [0, J_last]
+// (J_last >= rank(H) - 1: rank(H) pivots) holds the pair (J_last, J_last + 1)
+// of that run, which the run test rejects (unless J_last is the last
+// position). That is the saturated-posterior case: every key of |LLR| > 36.7
+// rounds to 1.0, configs[3] p = 0.1 status-2 shots hold ~870 such (median)
+// and certified ones ~0 (`profiles/r04ac/`). They go to NumPy's order at
+// once (status 2, posteriors spilled) instead of being eliminated twice; the
+// host path gives every shot its exact result either way. Only shots whose
+// first near-tie lies inside that prefix pay for the run-start scan.
+__device__ __forceinline__ bool osd_early_tie(const OsdArgs& a, long long shot, int n, int* slot) {
+  if (!a.tiepos || a.tiepos[shot] >= a.rank) return false;     // uniform per workgroup
+  if (threadIdx.x == 0) *slot = 0;
+  __syncthreads();
+  const double* post = a.post + shot * (long long)n;
+  const int32_t* perm = a.perm + shot * (long long)n;
+  int last = 0;                                               // 1 + the last position ending a key gap
+  for (int i = threadIdx.x; i + 1 < n; i += blockDim.x) {
+    const uint64_t k0 = order_key(post[perm[i]]), k1 = order_key(post[perm[i + 1]]);
+    if (k0 == kBadKey || k1 == kBadKey || k1 - k0 > (uint64_t)kOrderMarginUlp) last = max(last, i + 1);
+  }
+  if (last) atomicMax(slot, last);
+  __syncthreads();
+  const int run_start = *slot;
+  __syncthreads();
+  if (run_start > a.rank - 1) return false;
+  if (threadIdx.x == 0) a.status[shot] = 2;
+  spill_shot(a, shot, n, slot);
+  return true;
+}
 
 // s_getreg immediates: (size - 1) << 11 | offset << 6 | register id
 constexpr int kHwRegHwId = (31 << 11) | 4;    // HW_ID: SIMD bits 4-5, CU 8-11, SH 12, SE 13-15
@@ -88,6 +119,7 @@ __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
   const int lane = t & 63, wave = t >> 6, nwaves = blockDim.x >> 6;
   const long long shot = blockIdx.x;
   if (a.redo && a.status[shot] != 3) return;       // second pass after osd_block_kernel
+  if (!a.redo && osd_early_tie(a, shot, n, slots)) return;
   const int32_t* perm = a.perm + shot * (long long)n;
   const uint8_t* syn = a.syn + shot * (long long)m;
   uint8_t* ehat = a.ehat + shot * (long long)n;
@@ -481,6 +513,7 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
   // branch is scalar and the counters it updates stay in SGPRs
   const int lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const long long shot = blockIdx.x;
+  if (osd_early_tie(a, shot, n, misc + 7)) return;
   const int32_t* perm = a.perm + shot * (long long)n;
   const uint8_t* syn = a.syn + shot * (long long)m;
   uint8_t* ehat = a.ehat + shot * (long long)n;

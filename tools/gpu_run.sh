@@ -12,6 +12,7 @@
 #   roof-hbm       counter profile of the HBM-resident kernel on the headline workload
 #   sim3 / sim4    tools/bench_sim.py p-sweep of configs[3] / configs[4]
 #   phases3/4      tools/prof_sim.py phase times of one configs[3] / configs[4] p = 0.1 batch
+#   ties           tools/osd_tie_stats.py: near-tie positions by OSD status (configs[3] p = 0.1)
 #   cfg3prof       per-kernel counters of one configs[3] p = 0.1 batch (tools/gpu_profile_program.sh)
 #   osd            tools/osd_bench.py on the configs[3] p = 0.1 OSD shots
 #   osdab:LIBS     interleaved A/B of the device OSD (tools/osd_bench.py, configs[3] p = 0.1) over library builds
@@ -97,6 +98,10 @@ for l in open('$L'):
     phases4b)
       L=$O/${TAG}_phases4b.json
       timeout -k 10 300 python -u tools/prof_sim.py LP118_2 BP L 4 100 0.1 262144 > $L 2>&1 || fail $step $? $L ;;
+    ties)
+      L=$O/${TAG}_ties.json
+      timeout -k 10 200 python -u tools/osd_tie_stats.py LP118_2 MS L 50 0.1 131072 > $L 2>&1 || fail $step $? $L
+      tail -1 $L | cut -c1-400 ;;
     cfg3prof)
       bash tools/gpu_profile_program.sh ${TAG}_cfg3 tools/prof_sim.py LP118_2 MS L 0 50 0.1 131072 || fail $step $? ;;
     osd)
