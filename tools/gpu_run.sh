@@ -13,6 +13,7 @@
 #   sim3 / sim4    tools/bench_sim.py p-sweep of configs[3] / configs[4]
 #   phases3/4      tools/prof_sim.py phase times of one configs[3] / configs[4] p = 0.1 batch
 #   ties           tools/osd_tie_stats.py: near-tie positions by OSD status (configs[3] p = 0.1)
+#   cfg3trace      rocprofv3 kernel trace + stats of tools/prof_sim.py on configs[3] p = 0.1
 #   cfg3prof       per-kernel counters of one configs[3] p = 0.1 batch (tools/gpu_profile_program.sh)
 #   osd            tools/osd_bench.py on the configs[3] p = 0.1 OSD shots
 #   osdab:LIBS     interleaved A/B of the device OSD (tools/osd_bench.py, configs[3] p = 0.1) over library builds
@@ -102,6 +103,12 @@ for l in open('$L'):
       L=$O/${TAG}_ties.json
       timeout -k 10 200 python -u tools/osd_tie_stats.py LP118_2 MS L 50 0.1 131072 > $L 2>&1 || fail $step $? $L
       tail -1 $L | cut -c1-400 ;;
+    cfg3trace)
+      D=$O/${TAG}_cfg3trace
+      mkdir -p $D
+      (export TMPDIR=/tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o t -- \
+        python3 tools/prof_sim.py LP118_2 MS L 0 50 0.1 131072 > $D/run.log 2>&1) || fail $step $? $D/run.log
+      tail -1 $D/run.log | cut -c1-300 ;;
     cfg3prof)
       bash tools/gpu_profile_program.sh ${TAG}_cfg3 tools/prof_sim.py LP118_2 MS L 0 50 0.1 131072 || fail $step $? ;;
     osd)
