@@ -362,3 +362,17 @@ def test_two_ranks_configs3_pipeline_counters_exact(tmp_path, device_min):
     assert abs(got["Avg_number_of_iterations_X"] - its[0] / shots) < 1e-9
     assert abs(got["Avg_number_of_iterations_Z"] - its[1] / shots) < 1e-9
     assert capped > 50                                      # OSD ran on many shots of both ranks
+
+
+def test_device_pipeline_counters_independent_of_batching():
+    """The device pipeline's tail batches are halved when OSD is a large
+    share of a batch (simulate_p): shots keep the sampler's indices, so the
+    counters of a sweep point are the same whatever the batch sequence —
+    here one batch, full batches, and full batches plus the tapered tail
+    (LP04_0 MS-L + OSD-0 at p = 0.12: most half-shots need OSD)."""
+    from qldpcsim_amd import codes, simulator
+    Hx, Hz = codes.load_code("LP04_0")
+    kw = dict(shots=3000, decType="MS", decIterations=30, decSchedule="L", OSDorder=0, rngSeed=5,
+              verbose=False, sampler="device")
+    runs = [simulator.simulate_p(Hx, Hz, 0.12, batch_size=b, **kw) for b in (3000, 1000, 512)]
+    assert runs[0] == runs[1] == runs[2], runs
