@@ -14,7 +14,7 @@
 #   phases3/4      tools/prof_sim.py phase times of one configs[3] / configs[4] p = 0.1 batch
 #   ties           tools/osd_tie_stats.py: near-tie positions by OSD status (configs[3] p = 0.1)
 #   cfg3trace      rocprofv3 kernel trace + stats of tools/prof_sim.py on configs[3] p = 0.1
-#   sim3trace      rocprofv3 kernel + copy trace of one configs[3] p = 0.1 simulate_p run (tools/sim_one.py)
+#   sim3trace      rocprofv3 kernel + copy trace of one configs[3] p = 0.1 simulate_p run (tools/bench_sim_one.py)
 #   cfg3prof       per-kernel counters of one configs[3] p = 0.1 batch (tools/gpu_profile_program.sh)
 #   osd            tools/osd_bench.py on the configs[3] p = 0.1 OSD shots
 #   osdab:LIBS     interleaved A/B of the device OSD (tools/osd_bench.py, configs[3] p = 0.1) over library builds
@@ -114,7 +114,7 @@ for l in open('$L'):
       D=$O/${TAG}_sim3trace
       mkdir -p $D
       (export TMPDIR=/tmp; timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $D -o t -- \
-        python3 tools/sim_one.py LP118_2 MS L 0 50 0.1 1048576 > $D/run.log 2>&1) || fail $step $? $D/run.log
+        python3 tools/bench_sim_one.py LP118_2 MS L 0 50 0.1 1048576 > $D/run.log 2>&1) || fail $step $? $D/run.log
       tail -1 $D/run.log | cut -c1-200 ;;
     cfg3prof)
       bash tools/gpu_profile_program.sh ${TAG}_cfg3 tools/prof_sim.py LP118_2 MS L 0 50 0.1 131072 || fail $step $? ;;

@@ -53,4 +53,4 @@ t = float(np.median(times))
 print(json.dumps({"code": code, "dec": dec, "sched": sched, "p": p, "B": B, "order": order,
                   "osd_shots": k, "sec": t, "osd_shots_per_s": k / t, "status_hist": hist, "ehat_sha": ehat_sha,
                   "lib": os.path.basename(_lib.LIB_PATH),
-                  "kernel": os.environ.get("QLDPC_OSD_KERNEL", "block")}))
+                  "kernel": "column" if _lib.get_option("osd_column") else "block"}))
