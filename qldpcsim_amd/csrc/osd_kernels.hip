@@ -607,6 +607,9 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
     __syncthreads();
     QLDPC_TICK(1);
     if (wave == engine) {                             // B
+      // The engine is its shot's critical path while the SIMD also runs
+      // other shots' phase-D waves: raised priority lets it issue first.
+      if constexpr (QLDPC_OSD_PRIO != 0) __builtin_amdgcn_s_setprio(QLDPC_OSD_PRIO);
       // the engine works on the rows still free (no pivot yet), compacted:
       // crow[c] = the c-th free row; earlier pivots are reduced in phase D
       const int rank0 = rank;
@@ -677,6 +680,7 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
           misc[7] = (int)(uint32_t)(pivm >> 32);
         }
       }
+      if constexpr (QLDPC_OSD_PRIO != 0) __builtin_amdgcn_s_setprio(0);
     }
     QLDPC_TICK(2);
     __syncthreads();

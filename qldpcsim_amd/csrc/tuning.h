@@ -12,7 +12,7 @@
     (defined(QLDPC_ABLATE) || defined(QLDPC_ABLATE_L) || defined(QLDPC_ABLATE_OSD) ||               \
      defined(QLDPC_OSD_TIMING) || defined(QLDPC_VN_PAIR) || defined(QLDPC_FLOOD_WPE) ||             \
      defined(QLDPC_VN_H) || defined(QLDPC_HBM_WAVES) || defined(QLDPC_HBM_UC) ||                    \
-     defined(QLDPC_OSD_WPE))
+     defined(QLDPC_OSD_WPE) || defined(QLDPC_OSD_PRIO))
 #error "kernel tuning knobs are for experiment builds: add -DQLDPC_EXPERIMENTS"
 #endif
 
@@ -48,4 +48,8 @@
 #endif
 #ifndef QLDPC_OSD_WPE
 #define QLDPC_OSD_WPE 4      // osd_block_kernel, two rows per thread: waves per SIMD (3: no spills, slower)
+#endif
+#ifndef QLDPC_OSD_PRIO
+#define QLDPC_OSD_PRIO 3     // osd_block_kernel: s_setprio of the engine wave during phase B (0: none;
+                             // 1 and 3 both -3.3 % per launch, profiles/r04am/)
 #endif
