@@ -116,13 +116,16 @@ def device_code_sha(path):
 def _demangle_kernel(sym):
     """'_ZN5qldpc15ms_flood_kernelILi8ELi4EEEvNS_10DecodeArgsE' -> 'ms_flood_kernel<8, 4>'
     (the kernel names rocprofv3 prints for this library's templates: int and
-    bool non-type arguments only); None for anything else."""
+    bool non-type arguments only); '_ZN5qldpc16osd_order_kernelENS_9OrderArgsE'
+    -> 'osd_order_kernel'; None for anything else."""
     m = re.match(r"_ZN5qldpc(\d+)", sym)
     if not m:
         return None
     i = m.end()
     name = sym[i:i + int(m.group(1))]
     i += int(m.group(1))
+    if sym[i:i + 1] == "E":
+        return name
     if sym[i:i + 1] != "I":
         return None
     i += 1

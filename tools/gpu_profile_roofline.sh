@@ -2,6 +2,7 @@
 # kernel-trace --stats pass and one --pmc pass per counter set, each a separate
 # short bench.py run (same seeds, so the same work) with its own worklog.
 # usage: bash tools/gpu_profile_roofline.sh TAG NAME "BENCH ARGS" [NAME "BENCH ARGS" ...]
+#        ("osd:ARGS" profiles tools/osd_bench.py ARGS instead of bench.py)
 #        then (here or there) python tools/roofline_profile.py TAG
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -18,7 +19,11 @@ while [ $# -ge 2 ]; do
   D=gpurun_out/roof_$TAG/$NAME
   mkdir -p $D
   echo "$ARGS" > $D/config.txt
-  BENCH="python3 bench.py --gpus 1 --steps 2 --warmup 1 --cpu-seconds 0 $ARGS"
+  if [[ "$ARGS" == osd:* ]]; then
+    BENCH="python3 tools/osd_bench.py ${ARGS#osd:}"
+  else
+    BENCH="python3 bench.py --gpus 1 --steps 2 --warmup 1 --cpu-seconds 0 $ARGS"
+  fi
   echo "[$NAME] trace"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o t -- $BENCH --worklog $D/trace.work.json > $D/trace.log 2>&1 || { echo "trace failed rc=$?"; exit 1; }
   i=0

@@ -8,6 +8,7 @@
 #   bench-cfg      bench.py on the configs[2]-[4] decoders    -> gpurun_out/TAG_bench_cfg.jsonl
 #   roof-decoders  counter profile (tools/gpu_profile_roofline.sh) of the configs[2]-[4] decoders
 #   roof-bp / roof-msl  counter profiles of the BP decoders / the layered MS decoder only
+#   roof-osd       counter profile of the device OSD kernels (tools/osd_bench.py, configs[3] p = 0.1)
 #   roof-flood     counter profile of the headline kernel
 #   roof-hbm       counter profile of the HBM-resident kernel on the headline workload
 #   sim3 / sim4    tools/bench_sim.py p-sweep of configs[3] / configs[4]
@@ -82,6 +83,8 @@ for l in open('$L'):
       bash tools/gpu_profile_roofline.sh ${TAG}b bpl2p10 "${CFG[bpl2p10]}" bpf0 "${CFG[bpf0]}" || fail $step $? ;;
     roof-msl)
       bash tools/gpu_profile_roofline.sh ${TAG}m msl2p05 "${CFG[msl2p05]}" msl2p10 "${CFG[msl2p10]}" || fail $step $? ;;
+    roof-osd)
+      bash tools/gpu_profile_roofline.sh ${TAG}o osd3p10 "osd:LP118_2 MS L 50 0.1 131072 0 2" || fail $step $? ;;
     roof-flood)
       bash tools/gpu_profile_roofline.sh ${TAG}f flood "" || fail $step $? ;;
     roof-hbm)

@@ -2,7 +2,10 @@
 simulate_p-style batch (device sampler, MS/BP decode with posteriors), then
 qldpc_osd_device_ordered (device order + elimination) timed over repeats,
 with the status histogram (2 = left to NumPy's order, 1 = IndexError case).
-usage: python tools/osd_bench.py CODE DEC SCHED ITERS P [B] [ORDER] [REPS]"""
+usage: python tools/osd_bench.py CODE DEC SCHED ITERS P [B] [ORDER] [REPS] [--worklog PATH]
+--worklog: every OSD call's kernels (family names, resolved against the
+rocprofv3 trace by tools/roofline_profile.py) with its shot count, the unit
+of a counter profile (tools/gpu_run.sh roof-osd)."""
 import json
 import os
 import sys
@@ -14,6 +17,11 @@ import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from qldpcsim_amd import _lib, codes, decoders, schedule, simulator  # noqa: E402
 
+worklog = None
+if "--worklog" in sys.argv:
+    i = sys.argv.index("--worklog")
+    worklog = sys.argv[i + 1]
+    del sys.argv[i:i + 2]
 code, dec, sched, it, p = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), float(sys.argv[5])
 B = int(sys.argv[6]) if len(sys.argv) > 6 else 65536
 order = int(sys.argv[7]) if len(sys.argv) > 7 else 0
@@ -46,6 +54,15 @@ for rep in range(reps + 1):
     torch.cuda.synchronize()
     if rep:
         times.append(time.perf_counter() - t)
+if worklog:
+    # one osd_order_kernel, one osd_block_kernel and one osd_kernel (the
+    # column kernel's redo pass) per call (capi.cpp osd_device_impl)
+    with open(worklog, "w") as f:
+        json.dump({"unit": "osd_shot",
+                   "launches": [{"kernel": kn, "half_shots": k, "iters": k}
+                                for _ in range(reps + 1)
+                                for kn in ("osd_order_kernel", "osd_block_kernel", "osd_kernel")
+                                if kn != "osd_block_kernel" or not _lib.get_option("osd_column")]}, f)
 hist = np.bincount(status.cpu().numpy(), minlength=4).tolist()
 import hashlib  # noqa: E402
 ehat_sha = hashlib.sha256(e.cpu().numpy().tobytes() + status.cpu().numpy().tobytes()).hexdigest()[:16]

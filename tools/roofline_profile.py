@@ -61,21 +61,41 @@ def stats(trace_dir, kernel):
     return None, 0
 
 
+def resolve(trace_dir, family):
+    """Full kernel name for a worklog entry: a family name without template
+    arguments (tools/osd_bench.py) is looked up in the trace's kernel names."""
+    if "<" in family:
+        return family
+    for fn in glob.glob(os.path.join(trace_dir, "**", "*kernel_stats.csv"), recursive=True):
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                nm = row["Name"]
+                for tail in ("<", "("):
+                    i = nm.find("::" + family + tail)
+                    if i >= 0:
+                        j = nm.find("(", i)
+                        return nm[i + 2:j]
+    return family
+
+
 def summarise_config(d):
     with open(os.path.join(d, "trace.work.json")) as f:
-        kernels = sorted({x["kernel"] for x in json.load(f)["launches"]})
+        wl = json.load(f)
+    kernels = sorted({x["kernel"] for x in wl["launches"]})
+    unit = wl.get("unit", "half_shot_iteration")
     meta = {}
     if os.path.exists(os.path.join(d, "config.txt")):
         meta["bench_args"] = open(os.path.join(d, "config.txt")).read().strip()
     out = []
-    for k in kernels:
+    for fam in kernels:
+        k = resolve(os.path.join(d, "trace"), fam)
         c = {}
         ok = True
         for p in sorted(glob.glob(os.path.join(d, "p*"))):
             if not os.path.isdir(p):
                 continue
             vals, nd = counters(p, k)
-            nl, hs, it = work(p + ".work.json", k)
+            nl, hs, it = work(p + ".work.json", fam)
             if nd != nl:
                 print(f"{p}: {nd} dispatches of {k} but the worklog has {nl}", file=sys.stderr)
                 ok = False
@@ -88,6 +108,8 @@ def summarise_config(d):
         import bench
         from qldpcsim_amd import _lib
         ent = {"kernel": k, **meta, "code_sha256": bench.kernel_code_sha(_lib.LIB_PATH, k),
+               **({"unit": unit + " (per_half_shot_iteration and per_half_shot are per " + unit + ")"}
+                  if unit != "half_shot_iteration" else {}),
                "per_half_shot_iteration": {
                    "valu_insts": per_it("SQ_INSTS_VALU"),
                    "lds_cycles": per_it("SQ_LDS_IDX_ACTIVE"),
@@ -136,11 +158,11 @@ def summarise_config(d):
         cyc = v / 8.0
         ent["busy"] = {"valu": c["SQ_ACTIVE_INST_VALU"][0] * 4 / 1024 / cyc,
                        "lds": c["SQ_LDS_IDX_ACTIVE"][0] / 256 / cyc,
-                       "lds_conflict_share": c["SQ_LDS_BANK_CONFLICT"][0] / c["SQ_LDS_IDX_ACTIVE"][0]}
+                       "lds_conflict_share": c["SQ_LDS_BANK_CONFLICT"][0] / max(c["SQ_LDS_IDX_ACTIVE"][0], 1.0)}
         ns, calls = stats(os.path.join(d, "trace"), k)
         ent["mean_duration_ns"] = ns
         ent["trace_calls"] = calls
-        tnl, ths, tit = work(os.path.join(d, "trace.work.json"), k)
+        tnl, ths, tit = work(os.path.join(d, "trace.work.json"), fam)
         if ns:
             # clock implied by the SQ pass's cycles at the trace pass's duration, per unit of work
             ent["clock_ghz"] = (cyc / it) / (ns * tnl / tit)
