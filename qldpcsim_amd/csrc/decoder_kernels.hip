@@ -1358,6 +1358,13 @@ __device__ __forceinline__ uint32_t vn_layer(const uint32_t* adj_info, const uin
 #pragma unroll
       for (int t = 0; t < K; ++t) x[h][t] = c[t];          // c2v padded by 8 floats
     }
+    // every read issued before any sum: left alone, the compiler turned a
+    // read whose value only feeds a select into an exec-masked read issued
+    // after all the others, behind a wait for everything in flight
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+#pragma unroll
+      for (int t = 0; t < K; ++t) asm volatile("" : "+v"(x[h][t]));
 #pragma unroll
     for (int h = 0; h < H; ++h) {
       const int d = (int)((info[h] >> 16) & 31u);
@@ -1404,9 +1411,15 @@ __device__ __forceinline__ void cn_layer(const DecodeArgs& a, const uint32_t* lt
       uint32_t t[1][8];
       load_row8(ltab + q * 8, t[0]);
       const int c = lrow[q];
-      const uint32_t sb[1] = {(synw[c >> 5] >> (c & 31)) & 1u};
+      // The row words and the check index go out in one LDS round trip, and
+      // the syndrome word with the messages: left alone, the compiler waited
+      // for the index before issuing the row reads and hoisted the syndrome
+      // read above the branch with a wait of its own (-1.4 % per launch on
+      // LP118_2 p = 0.1, profiles/r04aq/)
+      __builtin_amdgcn_sched_barrier(0);
       const bool live[1] = {true};
       if (first) {
+        const uint32_t sb[1] = {(synw[c >> 5] >> (c & 31)) & 1u};
         (void)cn_ms_uniform<DC, true, 1>(a, t, sb, live, (const unsigned char*)colS, c2v_b, fl);
       } else {
         CnLoad<DC> Ld;
@@ -1417,7 +1430,8 @@ __device__ __forceinline__ void cn_layer(const DecodeArgs& a, const uint32_t* lt
           Ld.pj[k] = a.L + (double)*QLDPC_LDS(const float, post_b + (t[0][k] & 0xffffu));   // (:173)
           Ld.cv[k] = *QLDPC_LDS(const float, ca[k]);
         }
-        (void)cn_ms_compute<DC>(a, Ld, ca, sb[0], 1u, fl);
+        const uint32_t sw = synw[c >> 5];
+        (void)cn_ms_compute<DC>(a, Ld, ca, (sw >> (c & 31)) & 1u, 1u, fl);
       }
     }
   } else {
