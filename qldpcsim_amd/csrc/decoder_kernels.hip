@@ -1334,19 +1334,15 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
 // QLDPC_VN_H (4: LP118_2's 240 / 480 in one / two passes instead of two / four,
 // -6.5 % per launch), smaller ones 2 (a 4-wide pass over <= 128 variables
 // idles half its lanes: LP118_0 +4 %)
-template <int K, int H>
+template <int K, int H, bool PRE>
 __device__ __forceinline__ uint32_t vn_layer(const uint32_t* adj_info, const uint32_t* avar, float* colS,
-                                             const float* c2v, int v0, int v1, int lane, float thr) {
+                                             const float* c2v, int v0, int v1, int lane, float thr,
+                                             const uint32_t* pre) {
   uint32_t acc = 0;
-  for (int qb = v0; qb < v1; qb += 64 * H) {
-    uint32_t info[H];
+  auto trip = [&](int qb, const uint32_t (&info)[H]) {
     bool in[H];
 #pragma unroll
-    for (int h = 0; h < H; ++h) {
-      const int q = qb + 64 * h + lane;
-      in[h] = q < v1;
-      info[h] = adj_info[in[h] ? q : v0];
-    }
+    for (int h = 0; h < H; ++h) in[h] = qb + 64 * h + lane < v1;
     float old[H];
     uint32_t av[H];
     float x[H][K];
@@ -1375,8 +1371,38 @@ __device__ __forceinline__ uint32_t vn_layer(const uint32_t* adj_info, const uin
       const bool flip = in[h] && ((old[h] < thr) != (s < thr));   // hard decision flipped (:173-174)
       acc ^= flip ? av[h] : 0u;
     }
+  };
+  int qb = v0;
+  if constexpr (PRE) {
+    // first trip: adjacency words read at the layer head (vn_preinfo)
+    static_assert(H <= 4, "vn_preinfo reads 4 words per lane");
+    if (v0 < v1) {                                          // (uniform)
+      uint32_t info[H];
+#pragma unroll
+      for (int h = 0; h < H; ++h) info[h] = pre[h];
+      trip(qb, info);
+      qb += 64 * H;
+    }
+  }
+  for (; qb < v1; qb += 64 * H) {
+    uint32_t info[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const int q = qb + 64 * h + lane;
+      info[h] = adj_info[q < v1 ? q : v0];
+    }
+    trip(qb, info);
   }
   return acc;
+}
+
+// the first VN trip's adjacency words (up to 4 per lane) of the layer [v0, v1)
+__device__ __forceinline__ void vn_preinfo(const uint32_t* adj_info, int v0, int v1, int lane, uint32_t (&pre)[4]) {
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    const int q = v0 + 64 * h + lane;
+    pre[h] = adj_info[q < v1 ? q : v0];
+  }
 }
 
 // Exact stop test (decoders.py:175-176): every row's parity of the current
@@ -1511,6 +1537,14 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
         const uint32_t dv = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uint32_t)adj_ptr[l] | ((uint32_t)adj_ptr[l + 1] << 16)));
         const int dsel = __builtin_amdgcn_readfirstlane((int)adj_dmax[l]);
         const int q0 = (int)(dq & 0xffffu), q1 = (int)(dq >> 16);
+        constexpr bool PRE = G == 1 && QLDPC_VN_PREINFO != 0;
+        uint32_t pre[4] = {0, 0, 0, 0};
+        if constexpr (PRE) {
+          // this layer's first VN adjacency words, in flight during the check
+          // nodes (the words never change); the one-lane-per-check instance only
+          const int pv0 = (int)(dv & 0xffffu), pv1 = (int)(dv >> 16);
+          if (pv0 < pv1) vn_preinfo(adj_info, pv0, pv1, lane, pre);
+        }
         if constexpr ((QLDPC_ABLATE_L & 1) != 0) {
         } else if constexpr (G != 0) {
           cn_layer<DC, G>(a, ltab, lrow, synw, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl);
@@ -1534,8 +1568,8 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
           case -1: break;
 #define QLDPC_VN_CASE(K)                                                                \
   case K:                                                                               \
-    acc = v1 - v0 > 128 ? vn_layer<K, QLDPC_VN_H>(adj_info, avar, colS, c2v, v0, v1, lane, thr) \
-                        : vn_layer<K, 2>(adj_info, avar, colS, c2v, v0, v1, lane, thr);        \
+    acc = v1 - v0 > 128 ? vn_layer<K, QLDPC_VN_H, PRE>(adj_info, avar, colS, c2v, v0, v1, lane, thr, pre) \
+                        : vn_layer<K, 2, PRE>(adj_info, avar, colS, c2v, v0, v1, lane, thr, pre);        \
     break;
           QLDPC_VN_CASE(3) QLDPC_VN_CASE(4) QLDPC_VN_CASE(5) QLDPC_VN_CASE(6)
 #undef QLDPC_VN_CASE

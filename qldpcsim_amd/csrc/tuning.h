@@ -12,7 +12,7 @@
     (defined(QLDPC_ABLATE) || defined(QLDPC_ABLATE_L) || defined(QLDPC_ABLATE_OSD) ||               \
      defined(QLDPC_OSD_TIMING) || defined(QLDPC_VN_PAIR) || defined(QLDPC_FLOOD_WPE) ||             \
      defined(QLDPC_VN_H) || defined(QLDPC_HBM_WAVES) || defined(QLDPC_HBM_UC) ||                    \
-     defined(QLDPC_OSD_WPE) || defined(QLDPC_OSD_PRIO))
+     defined(QLDPC_OSD_WPE) || defined(QLDPC_OSD_PRIO) || defined(QLDPC_VN_PREINFO))
 #error "kernel tuning knobs are for experiment builds: add -DQLDPC_EXPERIMENTS"
 #endif
 
@@ -52,4 +52,8 @@
 #ifndef QLDPC_OSD_PRIO
 #define QLDPC_OSD_PRIO 3     // osd_block_kernel: s_setprio of the engine wave during phase B (0: none;
                              // 1 and 3 both -3.3 % per launch, profiles/r04am/)
+#endif
+#ifndef QLDPC_VN_PREINFO
+#define QLDPC_VN_PREINFO 1     // ms_layered_kernel<DC, 1>: first VN adjacency words read at the layer head
+                               // (-0.85 % per LP118_2 p = 0.1 launch, profiles/r04as/)
 #endif
