@@ -1367,7 +1367,12 @@ __device__ __forceinline__ uint32_t vn_layer(const uint32_t* adj_info, const uin
       float s = 0.0f;                                       // sequential, ascending check (:172)
 #pragma unroll
       for (int t = 0; t < K; ++t) s += (t < d) ? x[h][t] : 0.0f;
-      if (in[h]) colS[info[h] >> 21] = s;
+      // every lane stores: a pad lane (past v1) holds variable v0's word and
+      // computes exactly the value v0's own lane stored (same reads — the
+      // c2v entries do not change in the VN — same sum), so no exec mask is
+      // needed around the store (-4.1 % per LP118_2 p = 0.1 launch,
+      // -4.9 % LP118_0, profiles/r04ax/)
+      colS[info[h] >> 21] = s;
       const bool flip = in[h] && ((old[h] < thr) != (s < thr));   // hard decision flipped (:173-174)
       acc ^= flip ? av[h] : 0u;
     }
