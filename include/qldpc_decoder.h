@@ -150,8 +150,7 @@ int qldpc_decode_host(const qldpc_code *code, const qldpc_schedule *sched, int a
  * order >= 2 -> identical to order 0. `h_ehat` (uint8[n]) is updated in place
  * like the reference's `e_hat[perm] = ...` (decoders.py:368).
  *   h_perm   int32[n]: np.argsort(reliability) as decoders.py:320-325 computes
- *            it. The caller computes it with NumPy so that NumPy's own exp and
- *            argsort decide near-ties exactly as in the reference.
+ *            it (NumPy itself, or qldpc_osd_order_host).
  *   h_J / h_J_size (nullable): the complementary information set (positions
  *            in perm order, decoders.py:329-342), h_J sized n.
  *   first_info_index: position the order-1 flip applies to (infoSet[0]);
@@ -177,22 +176,38 @@ int qldpc_osd_device(const qldpc_code *code, int64_t count, const uint8_t *d_syn
 
 /* The reliability order of decoders.py:320-325 on the device, for `count`
  * posterior rows d_post double[count][n] (n <= 2048): d_perm int32[count][n]
- * = the keys max(prob, 1 - prob), prob = 1/(1 + exp(clip(post, +-100))),
- * sorted ascending (index order among equal keys). NumPy's argsort orders
- * equal keys its own way and NumPy's exp may differ from the device's in the
- * last bits, so the order is only certified below d_tiepos[row]: the first
- * sorted position whose key gap to the next is within 64 units in the last
- * place (n if none; 0 if a posterior is NaN). No reference counterpart as an
- * entry point (it replaces the np.argsort call inside OSDdec). */
+ * = np.argsort of the keys max(prob, 1 - prob), prob = 1/(1 + np.exp(
+ * clip(post, +-100))), exactly as NumPy 2.2.6 computes them on x86-64
+ * AVX512_SKX: the key through SVML's exp8_ha (include/qldpc_libm.h), the order
+ * through x86-simd-sort's argsort, equal keys included (np_order.cpp states
+ * the algorithm). d_tiepos[row] = n for an exact order; -1 where this order
+ * leaves the row to NumPy itself (a NaN posterior, or x86-simd-sort's
+ * std::sort fallback after 2 floor(log2 n) partition levels). No reference
+ * counterpart as an entry point (it replaces the np.argsort call inside
+ * OSDdec, decoders.py:325). */
 int qldpc_osd_order_device(const qldpc_code *code, int64_t count, const double *d_post, int32_t *d_perm,
                            int32_t *d_tiepos, void *stream);
 
+/* The same order on the host (C++, `nthreads` threads): h_perm int32[count][n],
+ * h_status int32[count] = 0 exact, 1 left to NumPy (as tiepos -1 above).
+ * Used to check at import that the running NumPy dispatches to the restated
+ * functions (qldpcsim_amd/decoders.py), and by the host OSD path. */
+int qldpc_osd_order_host(const double *h_post, int64_t count, int n, int32_t *h_perm, int32_t *h_status,
+                         int nthreads);
+
+/* x86-simd-sort's argsort (np.argsort, default kind, float64) of n keys into
+ * h_perm; returns 0, or 1 for a case left to NumPy (NaN, std::sort fallback). */
+int qldpc_np_argsort_host(const double *h_key, int n, int32_t *h_perm);
+
+/* The reliability keys themselves (qldpc_osd_key), element-wise; exp_only != 0:
+ * np.exp alone (SVML exp8_ha restated, |x| < 707). */
+void qldpc_osd_keys_host(const double *h_post, int64_t count, double *h_key, int exp_only);
+
 /* qldpc_osd_device with the order computed on the device
  * (qldpc_osd_order_device into the caller's workspaces d_perm / d_tiepos):
- * a shot whose result depends on a part of the order that is not certified
- * (its elimination visited position tiepos, or the order-1 flip lies there)
- * gets d_status 2 and its e_hat is left unchanged: the caller decides it with
- * NumPy's order (qldpc_osd_device). Status 0 / 1 as qldpc_osd_device. */
+ * a shot whose order the device leaves to NumPy (tiepos -1) gets d_status 2
+ * and its e_hat is left unchanged: the caller decides it with NumPy's order
+ * (qldpc_osd_device). Status 0 / 1 as qldpc_osd_device. */
 int qldpc_osd_device_ordered(const qldpc_code *code, int64_t count, const uint8_t *d_syn, const double *d_post,
                              int order, uint8_t *d_ehat, int32_t *d_status, int32_t *d_perm, int32_t *d_tiepos,
                              void *stream);

@@ -249,11 +249,73 @@ QLDPC_HD double qldpc_atanh_t(double x, const double* hl, const uint32_t* rb) {
   return qldpc_atanh_x(x, hl, rb, 0);
 }
 
+/* np.exp (SVML __svml_exp8_ha, DOUBLE_exp_AVX512_SKX's loop for operands
+   that do not overlap) for |x| < QLDPC_EXP_RARE, NaN included (propagated);
+   hl = QLDPC_EXP_HL_INIT (2^(j/16) hi, lo pairs). SVML:
+     z = fma_rz(x, log2e, S)       S = 1.5 * 2^48 (+ 0x3ff0 ulps): z - S = k/16,
+                                   k = floor(16 x log2e) (rounding toward zero,
+                                   the sum being positive), j = k mod 16 = the
+                                   low 4 bits of z
+     r = (x - N ln2hi) - N ln2lo   N = z - S, two FMAs; bit 62 of r cleared
+     p = r (c0 + c1 r + ... + c5 r^5) + lo_j   (Estrin, as the SVML code)
+     exp(x) = scalef(hi_j p + hi_j, N) = (hi_j p + hi_j) * 2^floor(N)
+   The FMA in round-toward-zero is restated in round-to-nearest: z_rn, then
+   the sign of the exact x log2e + S - z_rn (one FMA: S - z_rn is exact, and
+   a round-to-nearest result keeps the sign of a nonzero exact value) says
+   whether z_rn lies above the exact sum, where z_rz is the next value down
+   (same binade: |x log2e| <= 1022 << 2^48). Used by the OSD reliability key
+   (decoders.py:323) only, whose clipped arguments lie in [-100, 100]. */
+QLDPC_HD double qldpc_np_exp_t(double x, const double* hl) {
+  const double S = qldpc_bits2d(QLDPC_EXP_SHIFTER_BITS);
+  if (x != x) return x;                          /* scalef(., NaN) = NaN */
+  const double zr = QLDPC_FMA(x, QLDPC_EXP_LOG2E, S);
+  const double below = QLDPC_FMA(x, QLDPC_EXP_LOG2E, S - zr);
+  const uint64_t zb = qldpc_d2bits(zr) - (below < 0.0 ? 1u : 0u);
+  const double N = qldpc_bits2d(zb) - S;                       /* k / 16, exact */
+  const int64_t k = (int64_t)(zb - QLDPC_EXP_SHIFTER_BITS);     /* (same binade) */
+  const int j = (int)(k & 15);
+  double r = QLDPC_FMA(-N, QLDPC_EXP_LN2HI, x);
+  r = QLDPC_FMA(-QLDPC_EXP_LN2LO, N, r);
+  r = qldpc_bits2d(qldpc_d2bits(r) & QLDPC_EXP_RMASK_BITS);
+  const double r2 = r * r;
+  double a = QLDPC_FMA(QLDPC_EXP_C5, r, QLDPC_EXP_C4);
+  const double b = QLDPC_FMA(QLDPC_EXP_C3, r, QLDPC_EXP_C2);
+  const double c = QLDPC_FMA(QLDPC_EXP_C1, r, QLDPC_EXP_C0);
+  a = QLDPC_FMA(a, r2, b);
+  a = QLDPC_FMA(a, r2, c);
+  const double hi = hl[2 * j], lo = hl[2 * j + 1];
+  const double p = QLDPC_FMA(r, a, lo);
+  const double res = QLDPC_FMA(hi, p, hi);
+  /* scalef by floor(N) = k >> 4: an exact power-of-two scaling (the result
+     is normal for |x| <= 700) */
+  int64_t e = k >> 4;
+  e = e < -1022 ? -1022 : (e > 1023 ? 1023 : e);
+  return res * qldpc_bits2d((uint64_t)(1023 + e) << 52);
+}
+
+/* The OSD reliability key of one posterior, NumPy's element for element
+   (decoders.py:320-324): sat = P if |P| < 100 else 100 sign(P) (NaN stays
+   NaN), prob = 1 / (1 + np.exp(sat)), key = prob if prob > 0.5 else 1 - prob.
+   Each step an IEEE-754 double operation in round-to-nearest (the divide and
+   add are NumPy's AVX-512 loops: correctly rounded). The key lies in
+   [0.5, 1] or is NaN. */
+QLDPC_HD double qldpc_osd_key_t(double P, const double* hl) {
+  const double aP = P < 0.0 ? -P : P;
+  const double sat = aP < 100.0 ? P : (P > 0.0 ? 100.0 : (P < 0.0 ? -100.0 : P));
+  const double t = 1.0 + qldpc_np_exp_t(sat, hl);
+  const double prob = 1.0 / t;
+  return prob > 0.5 ? prob : 1.0 - prob;
+}
+
 /* host image of the tables (the oracle, the library's host code; in HIP
    sources these are host functions, never emitted for the device) */
 static const qldpc_libm_tab qldpc_libm_host = QLDPC_LIBM_TAB_INIT;
 static const uint64_t qldpc_log_rcp_t[16] = QLDPC_LOG_RCP_T_INIT;
 static const double qldpc_log_ab[32] = QLDPC_LOG_AB_INIT;
+static const double qldpc_exp_hl[32] = QLDPC_EXP_HL_INIT;
+
+static inline double qldpc_np_exp(double x) { return qldpc_np_exp_t(x, qldpc_exp_hl); }
+static inline double qldpc_osd_key(double P) { return qldpc_osd_key_t(P, qldpc_exp_hl); }
 
 static inline double qldpc_tanh(double x) { return qldpc_tanh_t(x, qldpc_libm_host.tanh_c); }
 static inline double qldpc_atanh(double x) {

@@ -1547,8 +1547,6 @@ extern "C" int qldpc_osd_order_device(const qldpc_code* code, int64_t count, con
   a.perm = d_perm;
   a.tiepos = d_tiepos;
   a.n = n;
-  a.np2 = 2;
-  while (a.np2 < n) a.np2 <<= 1;
   HIP_TRY(qldpc::launch_osd_order(a, count, (hipStream_t)stream));
   return QLDPC_OK;
 }

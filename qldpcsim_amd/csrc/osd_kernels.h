@@ -11,13 +11,11 @@ struct OsdArgs {
   const int32_t* perm;     // [count][n] reliability order (NumPy argsort, decoders.py:325)
   const uint8_t* syn;      // [count][m]
   uint8_t* ehat;           // [count][n] in/out
-  int32_t* status;         // [count] 0 ok, 1 = reference IndexError case, 2 = order not certified
+  int32_t* status;         // [count] 0 ok, 1 = reference IndexError case, 2 = order left to the host
                            // (3 = internal: osd_block_kernel hands the shot to osd_kernel)
-  const int32_t* tiepos;   // [count] or null: first sorted position t whose key gap to t+1 is
-                           // within the certification margin (osd_order_kernel); with it, a
-                           // shot whose decision prefix reaches tiepos is left untouched (status 2)
-  const double* post;      // [count][n] posteriors behind tiepos' order (osd_block_kernel's
-                           // tie-run certification), with tiepos
+  const int32_t* tiepos;   // [count] or null: osd_order_kernel's verdict; -1 = the order is
+                           // left to NumPy on the host: the shot is left untouched (status 2)
+  const double* post;      // [count][n] posteriors (spilled for status-2 shots), with tiepos
   int m, n, rank, order;
   // status-2 spill (optional): a shot left to the host also copies its
   // posterior row to spill_post[slot] and its index to spill_idx[slot],
@@ -33,20 +31,17 @@ struct OsdArgs {
                            // (left by osd_block_kernel: syndrome outside H's column space)
 };
 
-// Reliability order on the device (decoders.py:320-325): keys
-// max(prob, 1 - prob), prob = 1 / (1 + exp(clip(post, +-100))), sorted
-// ascending (index order among equal keys) into perm; tiepos = the first
-// sorted position whose gap to the next key is <= kOrderMarginUlp units in
-// the last place (n if none, 0 for a non-finite posterior).
+// Reliability order on the device (decoders.py:320-325): NumPy's exact order
+// (osd_order_kernel); tiepos = n, or -1 where the host's NumPy must decide.
 struct OrderArgs {
   const double* post;      // [count][n]
   int32_t* perm;           // [count][n]
   int32_t* tiepos;         // [count]
-  int n, np2;              // np2 = power of two >= n (<= 2048)
+  int n;                   // <= 2048
 };
-constexpr int kOrderMarginUlp = 64;
 constexpr int kOsdCuSlots = 16 * 256;  // XCC id (4 bits) x HW_ID bits 8-15 (CU, SH, SE)
 hipError_t launch_osd_order(const OrderArgs& a, long long count, hipStream_t stream);
+size_t osd_order_lds(int n);
 
 const void* select_osd_kernel(int nw);  // nw = 64-bit words per row incl. the syndrome column
 const void* select_osd_block_kernel(int nw, int m, int* rows_per_thread);  // block elimination (default), same arguments

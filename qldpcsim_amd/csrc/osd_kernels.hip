@@ -26,25 +26,11 @@
 
 #include "osd_kernels.h"
 #include "tuning.h"
+#include "../../include/qldpc_libm.h"
 
 namespace qldpc {
 
 __device__ int first_setdiff(int n, const unsigned char* inJ, int nJ, int* table);
-
-// Sort key of one posterior as NumPy forms it in decoders.py:320-325 (clip,
-// exp, 1 / (1 + e), max(prob, 1 - prob)), with the device exp: the key lies
-// in [0.5, 1], so bits(key) - bits(0.5) (< 2^53) orders like the key itself.
-// kBadKey for a NaN posterior.
-constexpr uint64_t kBadKey = ~0ull;
-__device__ __forceinline__ uint64_t order_key(double x) {
-  x = x < -100.0 ? -100.0 : (x > 100.0 ? 100.0 : x);   // np.clip(P, -100, 100)
-  const double e = exp(x);
-  const double prob = 1.0 / (1.0 + e);
-  const double q = 1.0 - prob;
-  const double rel = prob > q ? prob : q;             // np.maximum(prob, 1 - prob)
-  if (!(rel >= 0.5 && rel <= 1.0)) return kBadKey;
-  return __builtin_bit_cast(uint64_t, rel) - 0x3FE0000000000000ull;   // bits of 0.5
-}
 
 // a status-2 shot's posterior row into the spill buffer (OsdArgs), whole
 // workgroup; `slot` is an LDS int the block may overwrite
@@ -60,33 +46,11 @@ __device__ __forceinline__ void spill_shot(const OsdArgs& a, long long shot, int
   if (threadIdx.x == 0) a.spill_idx[q] = (int32_t)(a.shot_base + shot);
 }
 
-// Shots whose certification (below) cannot succeed, told apart before the
-// elimination: when the run of near-tied keys that ends the device order
-// starts inside the first rank(H) positions, the decision prefix [0, J_last]
-// (J_last >= rank(H) - 1: rank(H) pivots) holds the pair (J_last, J_last + 1)
-// of that run, which the run test rejects (unless J_last is the last
-// position). That is the saturated-posterior case: every key of |LLR| > 36.7
-// rounds to 1.0, configs[3] p = 0.1 status-2 shots hold ~870 such (median)
-// and certified ones ~0 (`profiles/r04ac/`). They go to NumPy's order at
-// once (status 2, posteriors spilled) instead of being eliminated twice; the
-// host path gives every shot its exact result either way. Only shots whose
-// first near-tie lies inside that prefix pay for the run-start scan.
-__device__ __forceinline__ bool osd_early_tie(const OsdArgs& a, long long shot, int n, int* slot) {
-  if (!a.tiepos || a.tiepos[shot] >= a.rank) return false;     // uniform per workgroup
-  if (threadIdx.x == 0) *slot = 0;
-  __syncthreads();
-  const double* post = a.post + shot * (long long)n;
-  const int32_t* perm = a.perm + shot * (long long)n;
-  int last = 0;                                               // 1 + the last position ending a key gap
-  for (int i = threadIdx.x; i + 1 < n; i += blockDim.x) {
-    const uint64_t k0 = order_key(post[perm[i]]), k1 = order_key(post[perm[i + 1]]);
-    if (k0 == kBadKey || k1 == kBadKey || k1 - k0 > (uint64_t)kOrderMarginUlp) last = max(last, i + 1);
-  }
-  if (last) atomicMax(slot, last);
-  __syncthreads();
-  const int run_start = *slot;
-  __syncthreads();
-  if (run_start > a.rank - 1) return false;
+// Shots whose reliability order the device leaves to NumPy on the host
+// (osd_order_kernel's tiepos -1: a NaN posterior, or x86-simd-sort's
+// std::sort fallback): status 2, posteriors spilled, before any elimination.
+__device__ __forceinline__ bool osd_host_shot(const OsdArgs& a, long long shot, int n, int* slot) {
+  if (!a.tiepos || a.tiepos[shot] >= 0) return false;        // uniform per workgroup
   if (threadIdx.x == 0) a.status[shot] = 2;
   spill_shot(a, shot, n, slot);
   return true;
@@ -119,7 +83,7 @@ __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
   const int lane = t & 63, wave = t >> 6, nwaves = blockDim.x >> 6;
   const long long shot = blockIdx.x;
   if (a.redo && a.status[shot] != 3) return;       // second pass after osd_block_kernel
-  if (!a.redo && osd_early_tie(a, shot, n, slots)) return;
+  if (!a.redo && osd_host_shot(a, shot, n, slots)) return;
   const int32_t* perm = a.perm + shot * (long long)n;
   const uint8_t* syn = a.syn + shot * (long long)m;
   uint8_t* ehat = a.ehat + shot * (long long)n;
@@ -230,23 +194,6 @@ __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
     return;
   }
   __syncthreads();
-  if (a.tiepos) {
-    // device-computed order: the result depends only on perm[0 .. need]
-    // (the columns the elimination visited and, for order 1, the flipped
-    // position); it equals NumPy's order there unless a key gap inside that
-    // prefix is within the certification margin -> leave it to the host
-    if (t == 0) {
-      int need = Jl[nJ - 1];
-      if (a.order == 1 && nJ < n) need = max(need, first_setdiff(n, inJ, nJ, table));
-      misc[3] = a.tiepos[shot] <= need;
-    }
-    __syncthreads();
-    if (misc[3]) {
-      if (t == 0) a.status[shot] = 2;
-      spill_shot(a, shot, n, slots);
-      return;
-    }
-  }
   // information-set values e_I (e_perm = e_hat[perm], decoders.py:345):
   // one column per thread, words assembled by ballots (all loads in flight)
   for (int i0w = 64 * wave; i0w < 64 * NW; i0w += blockDim.x) {
@@ -513,7 +460,7 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
   // branch is scalar and the counters it updates stay in SGPRs
   const int lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const long long shot = blockIdx.x;
-  if (osd_early_tie(a, shot, n, misc + 7)) return;
+  if (osd_host_shot(a, shot, n, misc + 7)) return;
   const int32_t* perm = a.perm + shot * (long long)n;
   const uint8_t* syn = a.syn + shot * (long long)m;
   uint8_t* ehat = a.ehat + shot * (long long)n;
@@ -756,44 +703,9 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
     int i0 = -1;
     if (a.order == 1 && nJ < n) i0 = first_setdiff(n, inJ, nJ, table);   // (decoders.py:344)
     misc[2] = i0;
-    misc[5] = 0;
-    misc[6] = a.tiepos && a.tiepos[shot] <= max(Jl[nJ - 1], i0);
   }
   __syncthreads();
   const int i0 = misc[2];
-  if (misc[6]) {
-    // The device order may differ from NumPy's only inside runs of near-equal
-    // keys (adjacent gaps within the margin; NumPy's exp / tie order can
-    // permute a run). The result stands if every such run that meets the
-    // decision prefix lies inside the eliminated columns [0, J_last], holds
-    // neither position 0 (always in J) nor the order-1 flip position, and is
-    // all-pivot or all-non-pivot: then every order of the run gives the same
-    // set J (an all-pivot run is independent modulo the columns before it, an
-    // all-non-pivot run lies in their span) and the same e (the solution of
-    // the same system). Anything else: status 2, NumPy's order on the host.
-    const int jlast = Jl[nJ - 1];
-    uint64_t* key = PW;                               // n keys (PW is free: 512 NW >= 8 n bytes)
-    bool fail = false;
-    for (int i = t; i < n; i += blockDim.x) {
-      const uint64_t k = order_key(a.post[shot * (long long)n + perm[i]]);
-      fail |= k == kBadKey;
-      key[i] = k;
-    }
-    __syncthreads();
-    for (int i = t; i + 1 < n; i += blockDim.x) {
-      if (key[i + 1] - key[i] > (uint64_t)kOrderMarginUlp) continue;   // not a near-tie pair
-      const bool flip = i == i0 || i + 1 == i0;
-      if (i > jlast) fail |= flip;                    // both outside J: only the flip position
-      else fail |= i == 0 || i + 1 > jlast || inJ[i] != inJ[i + 1] || flip;
-    }
-    if (fail) misc[5] = 1;
-    __syncthreads();
-    if (misc[5]) {
-      if (t == 0) a.status[shot] = 2;
-      spill_shot(a, shot, n, misc + 7);
-      return;
-    }
-  }
   if (misc[3]) {
     if (t == 0) a.status[shot] = 3;
     return;
@@ -825,59 +737,277 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
 }
 
 // ---------------------------------------------------------------------------
-// Reliability order of one shot per workgroup (np2 / 2 threads): keys as
-// NumPy forms them in decoders.py:320-325 (clip, exp, 1 / (1 + e),
-// max(prob, 1 - prob)), with the device exp; a key lies in [0.5, 1], so
-// (bits - bits(0.5)) fits 53 bits and (that << 11 | index) sorts by key, then
-// index, as one 64-bit integer (bitonic network in LDS). NumPy's argsort
-// breaks ties its own way and its exp may differ from the device's in the
-// last bits, so the caller trusts this order only up to tiepos (the first
-// adjacent pair closer than kOrderMarginUlp units in the last place).
+// Reliability order of one shot per workgroup: NumPy's own (decoders.py:
+// 320-325), bit for bit and tie for tie. Keys by qldpc_osd_key_t (SVML exp8_ha
+// restated, include/qldpc_libm.h); the order by x86-simd-sort's argsort as
+// NumPy 2.2.6 dispatches it on AVX512_SKX (np_order.cpp states the algorithm,
+// its host twin). The quicksort levels (segments > 256 keys) run one segment
+// at a time over the whole workgroup:
+//   * thread 0: the pivot (5th smallest of 8 samples) and the (size % 32)
+//     scalar steps, which swap keys >= pivot to the segment's end;
+//   * every thread: the >= pivot flag of each key of the 32-aligned middle,
+//     per 8-key vector a ballot byte;
+//   * wave 0: the block schedule — which 32-key block x86-simd-sort loads at
+//     each step (left or right end, decided by the store counts so far) — as a
+//     scalar loop over the blocks' counts held in lanes (readlane), giving each
+//     vector its store offsets (lt keys at l_store, ge keys below r_store + 8);
+//   * every thread: each key to its slot (lane order within the vector).
+// Segments of <= 256 keys are sorted together at the end: the bitonic network
+// of argsort_n (flip + half-cleaner stages over max(8, 2^ceil) slots, virtual
+// +inf pads, comparators that never move equal keys), one stage per barrier
+// for all of them at once. tiepos = n for an exact order, -1 where NumPy's
+// order is left to the host: a NaN key, or x86-simd-sort's std::sort fallback
+// after 2 floor(log2 n) partition levels (not restated).
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(1024) osd_order_kernel(OrderArgs a) {
+__constant__ double kExpHL[32] = QLDPC_EXP_HL_INIT;
+
+constexpr int kOrdThreads = 256;
+constexpr int kOrdMaxPer = 2048 / kOrdThreads;         // middle keys per thread (n <= 2048)
+
+__global__ void __launch_bounds__(kOrdThreads) osd_order_kernel(OrderArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  uint64_t* key = (uint64_t*)lds;                   // [np2]
-  int* tmin = (int*)(lds + 8 * a.np2);               // [1]
-  const int t = threadIdx.x, nt = blockDim.x;
+  const int n = a.n;
+  double* key = (double*)lds;                                    // [n] by original index
+  double* pv = key + n;                                          // [1] pivot (+ pad)
+  uint32_t* seg = (uint32_t*)(pv + 2);                           // [n] small segment: start << 16 | len
+  int* lb = (int*)(seg + n);                                     // [256] per vector: lt store base
+  int* re = lb + 256;                                            // [256] per vector: ge store end
+  int* cnt = re + 256;                                           // [256] per vector: ge count
+  int* stk = cnt + 256;                                          // [16][4] (L, R, iters, -)
+  int* misc = stk + 64;                                          // [0] sp [1] fallback [2] left [3] right
+                                                                 // [4] pidx [5] lt_any [6] gt_any [7] maxP
+                                                                 // [8..11] small children (L, len) x2
+  uint16_t* arg = (uint16_t*)(misc + 16);                        // [n] current arrangement
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const long long shot = blockIdx.x;
-  const double* post = a.post + shot * (long long)a.n;
-  const int n = a.n, np2 = a.np2;
-  bool bad = false;
-  for (int i = t; i < np2; i += nt) {
-    uint64_t c = ~0ull;                               // padding sorts last
-    if (i < n) {
-      const uint64_t u = order_key(post[i]);
-      if (u == kBadKey) bad = true;                   // NaN posterior: host decides
-      c = ((u & ((1ull << 53) - 1)) << 11) | (uint64_t)i;
-    }
-    key[i] = c;
+  const double* post = a.post + shot * (long long)n;
+  int32_t* perm = a.perm + shot * (long long)n;
+
+  bool nan = false;
+  for (int i = t; i < n; i += kOrdThreads) {
+    const double k = qldpc_osd_key_t(post[i], kExpHL);
+    nan |= k != k;
+    key[i] = k;
+    arg[i] = (uint16_t)i;
+    seg[i] = n <= 256 ? (uint32_t)n : 0u;
   }
-  if (t == 0) *tmin = n;
-  __syncthreads();
-  for (int k = 2; k <= np2; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = t; i < np2 / 2; i += nt) {
-        const int lo = 2 * i - (i & (j - 1)), hi = lo + j;
-        const bool up = (lo & k) == 0;
-        const uint64_t x = key[lo], y = key[hi];
-        if ((x > y) == up) {
-          key[lo] = y;
-          key[hi] = x;
+  int lg = 0;
+  while ((2 << lg) <= n) ++lg;                                   // floor(log2 n)
+  if (t == 0) {
+    misc[0] = 0;
+    misc[1] = 0;
+    misc[7] = 8;
+    if (n > 256) {
+      stk[0] = 0;
+      stk[1] = n - 1;
+      stk[2] = 2 * lg;
+      misc[0] = 1;
+    } else {
+      int P = 8;
+      while (P < n) P <<= 1;
+      misc[7] = P;
+    }
+  }
+  if (__syncthreads_or(nan)) {
+    for (int i = t; i < n; i += kOrdThreads) perm[i] = i;
+    if (t == 0) a.tiepos[shot] = -1;                             // std_argsort_withnan: host
+    return;
+  }
+
+  // ---- quicksort levels: argsort_64bit_ / argpartition_unrolled<4> ----
+  while (true) {
+    const int sp = misc[0];
+    if (sp == 0 || misc[1]) break;
+    const int L = stk[4 * (sp - 1)], R = stk[4 * (sp - 1) + 1], it = stk[4 * (sp - 1) + 2];
+    __syncthreads();                                             // everyone has read the top
+    if (t == 0) {
+      misc[0] = sp - 1;
+      const int q = (R - L) >> 3;
+      double sm[8];
+      for (int i = 0; i < 8; ++i) sm[i] = key[arg[L + q * (i + 1)]];
+      for (int i = 1; i < 8; ++i) {                              // the sample's 5th smallest
+        const double v = sm[i];
+        int j = i - 1;
+        while (j >= 0 && sm[j] > v) {
+          sm[j + 1] = sm[j];
+          --j;
+        }
+        sm[j + 1] = v;
+      }
+      const double pivot = sm[4];
+      int left = L, right = R + 1, lt = 0, gt = 0;
+      for (int i = (right - left) % 32; i > 0; --i) {            // scalar steps from the left
+        const uint16_t x = arg[left];
+        const double v = key[x];
+        lt |= v < pivot;
+        gt |= v > pivot;
+        if (!(v < pivot)) {
+          --right;
+          arg[left] = arg[right];
+          arg[right] = x;
+        } else {
+          ++left;
+        }
+      }
+      *pv = pivot;
+      misc[2] = left;
+      misc[3] = right;
+      misc[5] = lt;
+      misc[6] = gt;
+    }
+    __syncthreads();
+    const double pivot = *pv;
+    const int left = misc[2], right = misc[3];
+    const int M = right - left;                                  // multiple of 32, >= 256
+    uint16_t el[kOrdMaxPer];
+    uint32_t byte[kOrdMaxPer];
+    bool lt = false, gt = false;
+#pragma unroll
+    for (int i = 0; i < kOrdMaxPer; ++i) {
+      const int o = t + kOrdThreads * i;                         // a wave covers 64 consecutive keys
+      bool ge = false;
+      el[i] = 0;
+      if (o < M) {
+        el[i] = arg[left + o];
+        const double v = key[el[i]];
+        ge = v >= pivot;
+        lt |= v < pivot;
+        gt |= v > pivot;
+      }
+      const uint64_t bal = __ballot(ge);
+      byte[i] = (uint32_t)(bal >> (lane & 56)) & 0xffu;
+      if ((lane & 7) == 0 && o < M) cnt[o >> 3] = __builtin_popcount(byte[i]);
+    }
+    lt = __syncthreads_or(lt);
+    gt = __syncthreads_or(gt);                                   // (also orders the cnt writes)
+    if (wave == 0) {
+      // x86-simd-sort's block schedule, scalar: blocks 1 .. nb-2 from the left
+      // or the right, then the held-back first and last blocks
+      const int nb = M >> 5;
+      int g = 0;
+      if (lane < nb) g = cnt[4 * lane] + cnt[4 * lane + 1] + cnt[4 * lane + 2] + cnt[4 * lane + 3];
+      int lsto = __builtin_amdgcn_readfirstlane(left), rend = __builtin_amdgcn_readfirstlane(right);
+      int lp = lsto + 32, rp = rend - 32;
+      const int base = lsto;
+      int myl = 0, myr = 0;
+      for (int step = 0; step < nb; ++step) {
+        int b;
+        if (step < nb - 2) {
+          if (rend - rp < lp - lsto) {
+            rp -= 32;
+            b = (rp - base) >> 5;
+          } else {
+            b = (lp - base) >> 5;
+            lp += 32;
+          }
+        } else {
+          b = step == nb - 2 ? 0 : nb - 1;
+        }
+        b = __builtin_amdgcn_readfirstlane(b);
+        if (lane == b) {
+          myl = lsto;
+          myr = rend;
+        }
+        const int gb = __builtin_amdgcn_readlane(g, b);
+        lsto += 32 - gb;
+        rend -= gb;
+      }
+      if (lane < nb) {
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) {
+          const int v = 4 * lane + ii, c = cnt[v];
+          lb[v] = myl;
+          re[v] = myr;
+          myl += 8 - c;
+          myr -= c;
+        }
+      }
+      if (lane == 0) misc[4] = lsto;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kOrdMaxPer; ++i) {
+      const int o = t + kOrdThreads * i;
+      if (o < M) {
+        const int v = o >> 3, k = o & 7;
+        const uint32_t below = byte[i] & ((1u << k) - 1u);
+        const int dst = (byte[i] >> k) & 1u ? re[v] - __builtin_popcount(byte[i]) + __builtin_popcount(below)
+                                            : lb[v] + k - __builtin_popcount(below);
+        arg[dst] = el[i];
+      }
+    }
+    // children (pivot != smallest: left part; pivot != biggest: right part)
+    if (t == 0) {
+      const int pidx = misc[4];
+      const bool l_any = lt || misc[5], g_any = gt || misc[6];
+      int nsm = 0, sp2 = misc[0];
+      const int cl[2] = {L, pidx}, cr[2] = {pidx - 1, R};
+      const bool on[2] = {l_any, g_any};
+      for (int c = 0; c < 2; ++c) {
+        if (!on[c]) continue;
+        const int len = cr[c] - cl[c] + 1;
+        if (it - 1 <= 0) {
+          misc[1] = 1;                                           // std_argsort: host
+        } else if (len > 256) {
+          stk[4 * sp2] = cl[c];
+          stk[4 * sp2 + 1] = cr[c];
+          stk[4 * sp2 + 2] = it - 1;
+          ++sp2;
+        } else {
+          misc[8 + 2 * nsm] = cl[c];
+          misc[9 + 2 * nsm] = len;
+          ++nsm;
+          int P = 8;
+          while (P < len) P <<= 1;
+          misc[7] = max(misc[7], P);
+        }
+      }
+      for (int c = nsm; c < 2; ++c) misc[9 + 2 * c] = 0;
+      misc[0] = sp2;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int st = misc[8 + 2 * c], len = misc[9 + 2 * c];
+      for (int i = t; i < len; i += kOrdThreads) seg[st + i] = ((uint32_t)st << 16) | (uint32_t)len;
+    }
+    __syncthreads();
+  }
+  if (misc[1]) {
+    for (int i = t; i < n; i += kOrdThreads) perm[i] = arg[i];
+    if (t == 0) a.tiepos[shot] = -1;
+    return;
+  }
+
+  // ---- segments of <= 256 keys: argsort_n's bitonic network, all at once ----
+  const int maxP = misc[7];
+  for (int k = 2; k <= maxP; k <<= 1) {
+    for (int j = k; j >= 1; j = (j == k ? k >> 2 : j >> 1)) {  // flip(k), then half-cleaners k/4 .. 1
+      for (int p = t; p < n; p += kOrdThreads) {
+        const uint32_t info = seg[p];
+        const int len = (int)(info & 0xffffu), st = (int)(info >> 16);
+        if (len < 2) continue;
+        int P = 8;
+        while (P < len) P <<= 1;
+        if (k > P) continue;
+        const int x = p - st, y = j == k ? x ^ (k - 1) : x ^ j;
+        if (x < y && y < len) {
+          const uint16_t u = arg[st + x], w = arg[st + y];
+          if (key[w] < key[u]) {
+            arg[st + x] = w;
+            arg[st + y] = u;
+          }
         }
       }
       __syncthreads();
+      if (j == 1) break;
     }
   }
-  int first = bad ? 0 : n;
-  for (int i = t; i + 1 < n; i += nt)
-    if ((key[i + 1] >> 11) - (key[i] >> 11) <= (uint64_t)kOrderMarginUlp) first = min(first, i);
-  for (int off = 32; off > 0; off >>= 1) first = min(first, __shfl_xor(first, off, 64));
-  if ((t & 63) == 0) atomicMin(tmin, first);
-  int32_t* perm = a.perm + shot * (long long)n;
-  for (int i = t; i < n; i += nt) perm[i] = (int32_t)(key[i] & 2047u);
-  __syncthreads();
-  if (t == 0) a.tiepos[shot] = *tmin;
+  for (int i = t; i < n; i += kOrdThreads) perm[i] = arg[i];
+  if (t == 0) a.tiepos[shot] = n;
 }
+
+size_t osd_order_lds(int n) { return (size_t)14 * n + 16 + 3 * 256 * 4 + 64 * 4 + 16 * 4 + 16; }
 
 hipError_t launch_osd_order(const OrderArgs& a, long long count, hipStream_t stream) {
   long long done = 0;
@@ -888,9 +1018,8 @@ hipError_t launch_osd_order(const OrderArgs& a, long long count, hipStream_t str
     ai.perm = a.perm + done * a.n;
     ai.tiepos = a.tiepos + done;
     void* params[] = {(void*)&ai};
-    const size_t lds = (size_t)8 * a.np2 + 16;
-    hipError_t e = hipLaunchKernel((const void*)&osd_order_kernel, dim3((unsigned)g), dim3(a.np2 / 2), params,
-                                   lds, stream);
+    hipError_t e = hipLaunchKernel((const void*)&osd_order_kernel, dim3((unsigned)g), dim3(kOrdThreads), params,
+                                   osd_order_lds(a.n), stream);
     if (e != hipSuccess) return e;
     done += g;
   }

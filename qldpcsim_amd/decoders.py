@@ -12,11 +12,17 @@ many syndromes of one matrix in one kernel launch.
 
 All decoding runs through the HIP kernels (libqldpc_hip.so via the C ABI);
 there is no CPU fallback. OSD of the non-converged shots runs on the device
-(osd_kernels.hip: the reliability order, certified against NumPy's tie
-breaking, and a block GF(2) elimination); shots whose order the device
-cannot certify get NumPy's own order (decoders.py:320-325) on the host and
-the device elimination again. `OSDdec` / `apply_osd` are the single-shot and
-host entry points (host C++ elimination).
+(osd_kernels.hip: NumPy's reliability order of decoders.py:320-325 — SVML's
+exp and x86-simd-sort's argsort restated, ties included — and a block GF(2)
+elimination); the rare shots the device order leaves to NumPy (a NaN
+posterior, x86-simd-sort's std::sort fallback) get NumPy's own order on the
+host and the device elimination again. `OSDdec` / `apply_osd` are the
+single-shot and host entry points (host C++ elimination).
+
+The restated order is NumPy 2.2.6's on x86-64 AVX512_SKX (the reference's
+capture host). At import, `numpy_order_pinned()` compares it with the running
+NumPy on a fixed set of tie-heavy rows; if they differ (another NumPy build
+or ISA dispatch), every OSD order is NumPy's own, computed on the host.
 
 Deviations from the reference (documented in DESIGN.md §7):
   * layers=None means flooding (the reference raises AttributeError on
@@ -171,13 +177,70 @@ def osd_perm(posteriorLLRs):
     return np.argsort(reliability)
 
 
+def _pin_rows():
+    """Fixed posterior rows for numpy_order_pinned: saturated (long runs of
+    keys equal to 1.0), min-sum-quantised (many exact ties), +-x pairs, the
+    clip edges, and sizes on both sides of the 256-key network."""
+    rng = np.random.default_rng(20251226)
+    rows = []
+    L = np.log((1 - 0.1 / 3) / (0.1 / 3))
+    for n in (7, 175, 256, 257, 544, 1020, 2047):
+        P = rng.normal(0, 6, n)
+        P[rng.random(n) < 0.7] *= 1e3
+        rows.append(P)
+        rows.append(L + rng.integers(-6, 7, n).astype(np.float32) * np.float32(0.975))
+        Q = rng.normal(0, 2, n)
+        Q[1::4] = -Q[::4][:Q[1::4].size]
+        Q[:6] = [0.0, -0.0, 100.0, -100.0, 36.7, -36.7][:min(6, n)]
+        rows.append(Q)
+    return rows
+
+
+_PINNED_ORDER = []
+
+
+def numpy_order_pinned():
+    """Whether the running NumPy's reliability order (np.exp, np.argsort)
+    equals the restatement the device and the host library run
+    (qldpc_osd_order_host): checked once, on _pin_rows(), bit for bit."""
+    if not _PINNED_ORDER:
+        ok = True
+        try:
+            for P in _pin_rows():
+                P = np.ascontiguousarray(P, np.float64)
+                n = P.size
+                perm = np.empty(n, np.int32)
+                st = np.empty(1, np.int32)
+                _lib.check(_lib.lib.qldpc_osd_order_host(_lib.ptr(P), 1, n, _lib.ptr(perm), _lib.ptr(st), 1))
+                if st[0] != 0 or not np.array_equal(perm, osd_perm(P)):
+                    ok = False
+                    break
+        except (OSError, AttributeError, RuntimeError):
+            ok = False
+        _PINNED_ORDER.append(ok)
+    return _PINNED_ORDER[0]
+
+
 def osd_perms(post, nthreads=None):
     """Row-wise reliability orders (decoders.py:320-325) of a [k, n] posterior
-    block: NumPy's own exp / argsort, chunked over host threads (identical to
-    per-row calls; NumPy releases the GIL in these loops)."""
+    block. When the running NumPy is the pinned one (numpy_order_pinned), the
+    host library's restatement computes them (C++ threads, no GIL), and
+    NumPy only the rows it leaves (NaN, std::sort fallback); otherwise NumPy's
+    own exp / argsort, chunked over host threads (identical to per-row calls;
+    NumPy releases the GIL in these loops)."""
     post = np.asarray(post)
     if post.shape[0] == 0:
         return np.zeros((0, post.shape[1]), np.int32)
+    if numpy_order_pinned() and post.dtype == np.float64:
+        P = np.ascontiguousarray(post)
+        k, n = P.shape
+        out = np.empty((k, n), np.int32)
+        st = np.empty(k, np.int32)
+        _lib.check(_lib.lib.qldpc_osd_order_host(_lib.ptr(P), k, n, _lib.ptr(out), _lib.ptr(st),
+                                                 int(nthreads or hostcores.rank_cores())))
+        for r in np.flatnonzero(st):
+            out[r] = osd_perm(P[r])
+        return out
 
     def one(P):
         # the reference's reliability, element for element (tests pin the bits):
@@ -245,10 +308,10 @@ def _pinned(key, shape, dtype):
 def apply_osd_device(H, syn, res, order, stream=None):
     """GPU OSD for the non-converged shots of a device decode `res`
     (DecodeResult of torch tensors, with posteriors). The reliability order is
-    computed on the device and trusted where it provably equals NumPy's
-    (qldpc_osd_device_ordered); only the shots whose OSD depends on a near-tie
-    have their posteriors copied to the host for NumPy's own order. Updates
-    res.ehat in place. See apply_osd_device_many for several decodes at once."""
+    NumPy's, computed on the device (qldpc_osd_device_ordered); only the shots
+    it leaves to NumPy (NaN posteriors, x86-simd-sort's std::sort fallback)
+    have their posteriors copied to the host. Updates res.ehat in place. See
+    apply_osd_device_many for several decodes at once."""
     return apply_osd_device_many([(H, syn, res)], order, stream)[0]
 
 
@@ -264,16 +327,15 @@ def apply_osd_device_many(items, order, stream=None):
 
 # Where the OSD reliability order comes from (decoders.py:320-325):
 #   device_min  fewest non-converged shots of one decode for which the order
-#               is computed on the device. Below it NumPy orders them on the
-#               host in one pass: few shots cost the host little, the device
-#               order would add a round trip (status back, then the host pass
-#               anyway for the tie-holding shots), and at low p most OSD shots
-#               carry saturated posteriors, whose exact key ties send them to
-#               the host regardless (LP118_2 MS-L p = 0.05: 735 of 738);
-#   host_order  NumPy's order for every OSD shot (A/B reference).
+#               is computed on the device (below it: on the host, after a copy
+#               of their posteriors); the device order is NumPy's exact order,
+#               so the default is every decode;
+#   host_order  the host computes every OSD shot's order (A/B reference, and
+#               the setting whenever the running NumPy is not the pinned one:
+#               numpy_order_pinned() False).
 # Read once at import from QLDPC_OSD_DEVICE_MIN / QLDPC_OSD_HOST_ORDER (tools
 # start one process per setting); set_osd_policy / osd_policy change it.
-OSD_POLICY = {"device_min": int(os.environ.get("QLDPC_OSD_DEVICE_MIN", "4096")),
+OSD_POLICY = {"device_min": int(os.environ.get("QLDPC_OSD_DEVICE_MIN", "1")),
               "host_order": os.environ.get("QLDPC_OSD_HOST_ORDER", "") == "1"}
 
 
@@ -296,7 +358,7 @@ def osd_policy(**kw):
 
 
 def _host_order_only():
-    return OSD_POLICY["host_order"]
+    return OSD_POLICY["host_order"] or not numpy_order_pinned()
 
 
 def _device_order_min():
@@ -331,8 +393,8 @@ def osd_device_stage(items, stream=None, slot0=0, order=0):
     whose result the device order decides, with its status copied into a
     pinned host buffer. Shots that need NumPy's order (status 2) are finished
     by osd_device_finish. `slot0` selects the pinned buffer set (pipelined
-    callers alternate). OSD_POLICY["host_order"] (A/B only) or n > 2048 sends
-    every shot through NumPy's order, as osd_perms computes it."""
+    callers alternate). OSD_POLICY["host_order"] (A/B, or an unpinned NumPy)
+    or n > 2048 sends every shot through the host order (osd_perms)."""
     staged = []
     with _on_stream(stream):
         for slot, (H, syn, res) in enumerate(items):

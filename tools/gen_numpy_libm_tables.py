@@ -14,6 +14,11 @@ golden vectors were captured on; `numpy._core._multiarray_umath.__cpu_dispatch__
   * np.log (float64)     DOUBLE_log_AVX512_SKX -> __svml_log8_ha, data block
     __svml_dlog_ha_data_internal_avx512 (the prior L = np.log((1-p)/p),
     decoders.py:147 / :232).
+  * np.exp (float64)     DOUBLE_exp_AVX512_SKX -> __svml_exp8_ha for
+    non-overlapping operands (the OSD reliability key, decoders.py:323), data
+    block __svml_dexp_ha_data_internal_avx512: 2^(j/16) as hi (+0x00) and lo
+    (+0x80) tables, log2(e), the round-toward-zero shifter, ln2 hi / lo, a
+    degree-6 series and the rare-path threshold.
 The SVML kernels start from vrcp14pd rounded to a 4-bit mantissa (atanh:
 add-half-and-truncate; log: vrndscalepd, round-half-even). vrcp14pd depends
 on the top 18 mantissa bits of its input only; the rounded value is a
@@ -139,6 +144,7 @@ def main():
     tanh = tanh_table(syms, rd)
     at = rd(syms["__svml_datanh_ha_data_internal_avx512"], 0x500 // 8)
     lg = rd(syms["__svml_dlog_ha_data_internal_avx512"], 0x400 // 8)
+    ex = rd(syms["__svml_dexp_ha_data_internal_avx512"], 0x500 // 8)
     c = lambda blk, off: blk[off // 8]  # noqa: E731  (broadcast constants: lane 0)
     t_at = probe_thresholds(0)
     t_lg = probe_thresholds(1)
@@ -159,6 +165,7 @@ def main():
     L.append(" * tanh:   NumPy simd_tanh_f64 lut16x18 (loops_hyperbolic.dispatch.c.src), stored as [9][16][2] row pairs.")
     L.append(" * atanh:  __svml_atanh8_ha data (__svml_datanh_ha_data_internal_avx512).")
     L.append(" * log:    __svml_log8_ha data (__svml_dlog_ha_data_internal_avx512).")
+    L.append(" * exp:    __svml_exp8_ha data (__svml_dexp_ha_data_internal_avx512).")
     L.append(" * rcp:    mantissa thresholds of the rounded vrcp14pd step functions (probed on the capture host). */")
     L.append("#ifndef QLDPC_NUMPY_TABLES_H\n#define QLDPC_NUMPY_TABLES_H\n")
     L.append("/* [9][16][2]: row pair (2q, 2q+1) of interval i, rows = b, c0 .. c16 of")
@@ -191,6 +198,20 @@ def main():
     L.append("}")
     for off in range(0x100, 0x400, 0x40):
         L.append("#define QLDPC_LOG_C%03x %s" % (off, hexd(c(lg, off))))
+    L.append("/* [16][2]: 2^(j/16) as hi, lo (exp) */")
+    L.append("#define QLDPC_EXP_HL_INIT { \\")
+    for i in range(16):
+        L.append("  %s, %s, \\" % (hexd(ex[i]), hexd(ex[16 + i])))
+    L.append("}")
+    bits = lambda off: struct.unpack("<Q", struct.pack("<d", c(ex, off)))[0]  # noqa: E731
+    L.append("#define QLDPC_EXP_LOG2E %s" % hexd(c(ex, 0x100)))
+    L.append("#define QLDPC_EXP_SHIFTER_BITS 0x%016xull" % bits(0x140))
+    L.append("#define QLDPC_EXP_LN2HI %s" % hexd(c(ex, 0x180)))
+    L.append("#define QLDPC_EXP_LN2LO %s" % hexd(c(ex, 0x1c0)))
+    L.append("#define QLDPC_EXP_RMASK_BITS 0x%016xull" % bits(0x200))
+    for k, off in enumerate(range(0x240, 0x3c0, 0x40)):
+        L.append("#define QLDPC_EXP_C%d %s" % (5 - k, hexd(c(ex, off))))
+    L.append("#define QLDPC_EXP_RARE %s" % hexd(c(ex, 0x400)))
     L.append("\n#endif")
     open(OUT, "w").write("\n".join(L) + "\n")
     print("wrote", OUT)
