@@ -737,279 +737,315 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
 }
 
 // ---------------------------------------------------------------------------
-// Reliability order of one shot per workgroup: NumPy's own (decoders.py:
+// Reliability order of one shot per wavefront: NumPy's own (decoders.py:
 // 320-325), bit for bit and tie for tie. Keys by qldpc_osd_key_t (SVML exp8_ha
 // restated, include/qldpc_libm.h); the order by x86-simd-sort's argsort as
-// NumPy 2.2.6 dispatches it on AVX512_SKX (np_order.cpp states the algorithm,
-// its host twin). The quicksort levels (segments > 256 keys) run one segment
-// at a time over the whole workgroup:
-//   * thread 0: the pivot (5th smallest of 8 samples) and the (size % 32)
-//     scalar steps, which swap keys >= pivot to the segment's end;
-//   * every thread: the >= pivot flag of each key of the 32-aligned middle,
-//     per 8-key vector a ballot byte;
-//   * wave 0: the block schedule — which 32-key block x86-simd-sort loads at
-//     each step (left or right end, decided by the store counts so far) — as a
+// NumPy 2.2.6 dispatches it on AVX512_SKX (np_order.cpp states the algorithm
+// and is its host twin). LDS holds the keys and indices in their current
+// arrangement (both move together); segments come off a small stack:
+//   * > 256 keys (argpartition_unrolled<4>): the pivot (5th smallest of 8
+//     samples, every lane sorts the same 8); the (size % 32) scalar steps as a
+//     walk over two 32-lane streams (left end, right end) whose comparisons
+//     are one ballot — a scalar loop assigns each touched key its slot; the
+//     32-aligned middle as ballots per 64-key row (8 vectors); x86-simd-sort's
+//     block schedule (left or right end, by the store counts so far) as a
 //     scalar loop over the blocks' counts held in lanes (readlane), giving each
-//     vector its store offsets (lt keys at l_store, ge keys below r_store + 8);
-//   * every thread: each key to its slot (lane order within the vector).
-// Segments of <= 256 keys are sorted together at the end: the bitonic network
-// of argsort_n (flip + half-cleaner stages over max(8, 2^ceil) slots, virtual
-// +inf pads, comparators that never move equal keys), one stage per barrier
-// for all of them at once. tiepos = n for an exact order, -1 where NumPy's
-// order is left to the host: a NaN key, or x86-simd-sort's std::sort fallback
-// after 2 floor(log2 n) partition levels (not restated).
+//     8-key vector its store offsets; every key to its slot;
+//   * <= 256 keys (argsort_n): the bitonic network in registers, 4 keys per
+//     lane, flip + half-cleaner stages over max(8, 2^ceil) slots with +inf
+//     pads; comparators swap only when the upper key is strictly smaller.
+// tiepos = n for an exact order, -1 where NumPy's order is left to the host:
+// a NaN key, or x86-simd-sort's std::sort fallback after 2 floor(log2 n)
+// levels (not restated).
 // ---------------------------------------------------------------------------
 __constant__ double kExpHL[32] = QLDPC_EXP_HL_INIT;
 
-constexpr int kOrdThreads = 256;
-constexpr int kOrdMaxPer = 2048 / kOrdThreads;         // middle keys per thread (n <= 2048)
+// compare-exchange of two registers of one lane (positions lo < hi)
+__device__ __forceinline__ void ord_cx(double& klo, int& ilo, double& khi, int& ihi) {
+  const bool sw = khi < klo;
+  const double k = klo;
+  const int i = ilo;
+  klo = sw ? khi : klo;
+  ilo = sw ? ihi : ilo;
+  khi = sw ? k : khi;
+  ihi = sw ? i : ihi;
+}
 
-__global__ void __launch_bounds__(kOrdThreads) osd_order_kernel(OrderArgs a) {
+// within-lane stage: partner position x ^ m, m in {1, 2, 3}
+__device__ __forceinline__ void ord_within(double (&k)[4], int (&id)[4], int m) {
+  if (m == 1) {
+    ord_cx(k[0], id[0], k[1], id[1]);
+    ord_cx(k[2], id[2], k[3], id[3]);
+  } else if (m == 2) {
+    ord_cx(k[0], id[0], k[2], id[2]);
+    ord_cx(k[1], id[1], k[3], id[3]);
+  } else {
+    ord_cx(k[0], id[0], k[3], id[3]);
+    ord_cx(k[1], id[1], k[2], id[2]);
+  }
+}
+
+// cross-lane stage: partner position x ^ m, m >= 4: lane ^ lm (lm = m >> 2),
+// register r ^ M3 (M3 = m & 3); hb = the highest bit of lm decides which side
+// is the lower position
+template <int M3>
+__device__ __forceinline__ void ord_cross(double (&k)[4], int (&id)[4], int lm, int hb, int lane) {
+  const bool lo = (lane & hb) == 0;
+  double nk[4];
+  int ni[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const double pk = __shfl_xor(k[r ^ M3], lm, 64);
+    const int pi = __shfl_xor(id[r ^ M3], lm, 64);
+    const bool take = lo ? pk < k[r] : k[r] < pk;
+    nk[r] = take ? pk : k[r];
+    ni[r] = take ? pi : id[r];
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    k[r] = nk[r];
+    id[r] = ni[r];
+  }
+}
+
+// argsort_n on positions [L, L + N), N <= 256, in registers (K: keys by
+// original index, A: the arrangement)
+__device__ __forceinline__ void ord_small(const double* K, uint16_t* A, int L, int N, int lane) {
+  int P = 8;
+  while (P < N) P <<= 1;
+  double k[4];
+  int id[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int x = 4 * lane + r;
+    id[r] = A[L + (x < N ? x : 0)];
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const double v = K[id[r]];
+    k[r] = 4 * lane + r < N ? v : __builtin_inf();
+  }
+  for (int kk = 2; kk <= P; kk <<= 1) {
+    if (kk <= 4) ord_within(k, id, kk - 1);                   // flip(2) = x ^ 1, flip(4) = x ^ 3
+    else ord_cross<3>(k, id, (kk - 1) >> 2, kk >> 3, lane);   // flip(kk) = x ^ (kk - 1)
+    for (int j = kk >> 2; j >= 1; j >>= 1) {                  // half-cleaners kk/4 .. 1
+      if (j >= 4) ord_cross<0>(k, id, j >> 2, j >> 2, lane);
+      else ord_within(k, id, j);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int x = 4 * lane + r;
+    if (x < N) A[L + x] = (uint16_t)id[r];
+  }
+}
+
+__device__ __forceinline__ void ord_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int EPL>                                          // keys per lane capacity: n <= 64 EPL
+__global__ void __launch_bounds__(64) osd_order_kernel(OrderArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int n = a.n;
-  double* key = (double*)lds;                                    // [n] by original index
-  double* pv = key + n;                                          // [1] pivot (+ pad)
-  uint32_t* seg = (uint32_t*)(pv + 2);                           // [n] small segment: start << 16 | len
-  int* lb = (int*)(seg + n);                                     // [256] per vector: lt store base
-  int* re = lb + 256;                                            // [256] per vector: ge store end
-  int* cnt = re + 256;                                           // [256] per vector: ge count
-  int* stk = cnt + 256;                                          // [16][4] (L, R, iters, -)
-  int* misc = stk + 64;                                          // [0] sp [1] fallback [2] left [3] right
-                                                                 // [4] pidx [5] lt_any [6] gt_any [7] maxP
-                                                                 // [8..11] small children (L, len) x2
-  uint16_t* arg = (uint16_t*)(misc + 16);                        // [n] current arrangement
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  double* K = (double*)lds;                                  // [n] keys by original index
+  int* stk = (int*)(K + n);                                  // [32][3] (L, R, iters)
+  uint16_t* VL = (uint16_t*)(stk + 96);                      // [256] per vector: lt store base
+  uint16_t* VR = VL + 256;                                   // [256] per vector: ge store end
+  uint16_t* A = VR + 256;                                    // [n] the arrangement (indices)
+  const int lane = threadIdx.x;
   const long long shot = blockIdx.x;
   const double* post = a.post + shot * (long long)n;
   int32_t* perm = a.perm + shot * (long long)n;
 
   bool nan = false;
-  for (int i = t; i < n; i += kOrdThreads) {
+  for (int i = lane; i < n; i += 64) {
     const double k = qldpc_osd_key_t(post[i], kExpHL);
     nan |= k != k;
-    key[i] = k;
-    arg[i] = (uint16_t)i;
-    seg[i] = n <= 256 ? (uint32_t)n : 0u;
+    K[i] = k;
+    A[i] = (uint16_t)i;
   }
+  bool fallback = __ballot(nan) != 0;                        // std_argsort_withnan: the host's
   int lg = 0;
-  while ((2 << lg) <= n) ++lg;                                   // floor(log2 n)
-  if (t == 0) {
-    misc[0] = 0;
-    misc[1] = 0;
-    misc[7] = 8;
-    if (n > 256) {
+  while ((2 << lg) <= n) ++lg;                               // floor(log2 n)
+  int sp = 0;
+  if (n > 1 && !fallback) {
+    if (lane == 0) {
       stk[0] = 0;
       stk[1] = n - 1;
       stk[2] = 2 * lg;
-      misc[0] = 1;
-    } else {
-      int P = 8;
-      while (P < n) P <<= 1;
-      misc[7] = P;
     }
+    sp = 1;
   }
-  if (__syncthreads_or(nan)) {
-    for (int i = t; i < n; i += kOrdThreads) perm[i] = i;
-    if (t == 0) a.tiepos[shot] = -1;                             // std_argsort_withnan: host
-    return;
-  }
-
-  // ---- quicksort levels: argsort_64bit_ / argpartition_unrolled<4> ----
-  while (true) {
-    const int sp = misc[0];
-    if (sp == 0 || misc[1]) break;
-    const int L = stk[4 * (sp - 1)], R = stk[4 * (sp - 1) + 1], it = stk[4 * (sp - 1) + 2];
-    __syncthreads();                                             // everyone has read the top
-    if (t == 0) {
-      misc[0] = sp - 1;
-      const int q = (R - L) >> 3;
-      double sm[8];
-      for (int i = 0; i < 8; ++i) sm[i] = key[arg[L + q * (i + 1)]];
-      for (int i = 1; i < 8; ++i) {                              // the sample's 5th smallest
-        const double v = sm[i];
-        int j = i - 1;
-        while (j >= 0 && sm[j] > v) {
-          sm[j + 1] = sm[j];
-          --j;
-        }
-        sm[j + 1] = v;
-      }
-      const double pivot = sm[4];
-      int left = L, right = R + 1, lt = 0, gt = 0;
-      for (int i = (right - left) % 32; i > 0; --i) {            // scalar steps from the left
-        const uint16_t x = arg[left];
-        const double v = key[x];
-        lt |= v < pivot;
-        gt |= v > pivot;
-        if (!(v < pivot)) {
-          --right;
-          arg[left] = arg[right];
-          arg[right] = x;
-        } else {
-          ++left;
-        }
-      }
-      *pv = pivot;
-      misc[2] = left;
-      misc[3] = right;
-      misc[5] = lt;
-      misc[6] = gt;
+  ord_fence();
+  while (sp > 0 && !fallback) {
+    --sp;
+    const int L = __builtin_amdgcn_readfirstlane(stk[3 * sp]);
+    const int R = __builtin_amdgcn_readfirstlane(stk[3 * sp + 1]);
+    const int it = __builtin_amdgcn_readfirstlane(stk[3 * sp + 2]);
+    if (it <= 0) {                                           // argsort_64bit_: std_argsort
+      fallback = true;
+      break;
     }
-    __syncthreads();
-    const double pivot = *pv;
-    const int left = misc[2], right = misc[3];
-    const int M = right - left;                                  // multiple of 32, >= 256
-    uint16_t el[kOrdMaxPer];
-    uint32_t byte[kOrdMaxPer];
+    if (R + 1 - L <= 256) {
+      ord_small(K, A, L, R + 1 - L, lane);
+      ord_fence();
+      continue;
+    }
+    // ---- argpartition_unrolled<4> ----
+    const int q = (R - L) >> 3;
+    double sm[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sm[i] = K[A[L + q * (i + 1)]];
+#pragma unroll
+    for (int i = 1; i < 8; ++i)                              // (same data in every lane)
+#pragma unroll
+      for (int j = i; j > 0; --j) {
+        const double lo = sm[j - 1], hi = sm[j];
+        sm[j - 1] = lo < hi ? lo : hi;
+        sm[j] = lo < hi ? hi : lo;
+      }
+    const double pivot = sm[4];
     bool lt = false, gt = false;
-#pragma unroll
-    for (int i = 0; i < kOrdMaxPer; ++i) {
-      const int o = t + kOrdThreads * i;                         // a wave covers 64 consecutive keys
-      bool ge = false;
-      el[i] = 0;
-      if (o < M) {
-        el[i] = arg[left + o];
-        const double v = key[el[i]];
-        ge = v >= pivot;
-        lt |= v < pivot;
-        gt |= v > pivot;
-      }
-      const uint64_t bal = __ballot(ge);
-      byte[i] = (uint32_t)(bal >> (lane & 56)) & 0xffu;
-      if ((lane & 7) == 0 && o < M) cnt[o >> 3] = __builtin_popcount(byte[i]);
-    }
-    lt = __syncthreads_or(lt);
-    gt = __syncthreads_or(gt);                                   // (also orders the cnt writes)
-    if (wave == 0) {
-      // x86-simd-sort's block schedule, scalar: blocks 1 .. nb-2 from the left
-      // or the right, then the held-back first and last blocks
-      const int nb = M >> 5;
-      int g = 0;
-      if (lane < nb) g = cnt[4 * lane] + cnt[4 * lane + 1] + cnt[4 * lane + 2] + cnt[4 * lane + 3];
-      int lsto = __builtin_amdgcn_readfirstlane(left), rend = __builtin_amdgcn_readfirstlane(right);
-      int lp = lsto + 32, rp = rend - 32;
-      const int base = lsto;
-      int myl = 0, myr = 0;
-      for (int step = 0; step < nb; ++step) {
-        int b;
-        if (step < nb - 2) {
-          if (rend - rp < lp - lsto) {
-            rp -= 32;
-            b = (rp - base) >> 5;
-          } else {
-            b = (lp - base) >> 5;
-            lp += 32;
-          }
+    int left = L, right = R + 1;
+    const int rem = (R + 1 - L) & 31;
+    if (rem) {
+      // the scalar steps: examine the key at `left`; < pivot: it stays, left
+      // advances (the next key is the next of the left stream); >= pivot: it
+      // swaps with the key at --right (the right stream's next), which is
+      // examined next. Lane i < 32 holds left-stream key i (position L + i),
+      // lane 32 + i right-stream key i (position R - i).
+      const int pos = lane < 32 ? L + lane : R - (lane - 32);
+      const int iv = A[pos];
+      const double kv = K[iv];
+      const uint64_t ltm = __ballot(kv < pivot);
+      int cur = 0, dest = -1;
+      bool ex = false;
+      for (int s = 0; s < rem; ++s) {
+        if (lane == cur) ex = true;
+        if ((ltm >> cur) & 1ull) {
+          if (lane == cur) dest = left;
+          ++left;
+          cur = left - L;
         } else {
-          b = step == nb - 2 ? 0 : nb - 1;
-        }
-        b = __builtin_amdgcn_readfirstlane(b);
-        if (lane == b) {
-          myl = lsto;
-          myr = rend;
-        }
-        const int gb = __builtin_amdgcn_readlane(g, b);
-        lsto += 32 - gb;
-        rend -= gb;
-      }
-      if (lane < nb) {
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii) {
-          const int v = 4 * lane + ii, c = cnt[v];
-          lb[v] = myl;
-          re[v] = myr;
-          myl += 8 - c;
-          myr -= c;
+          --right;
+          if (lane == cur) dest = right;
+          cur = 32 + (R - right);
         }
       }
-      if (lane == 0) misc[4] = lsto;
+      if (lane == cur) dest = left;                          // moved to `left`, not examined
+      lt |= ex && kv < pivot;
+      gt |= ex && kv > pivot;
+      if (dest >= 0) A[dest] = (uint16_t)iv;
+      ord_fence();
     }
-    __syncthreads();
+    // the 32-aligned middle [left, right): rows of 64 keys (8 vectors)
+    const int M = right - left, nb = M >> 5;
+    int iv[EPL];
+    uint32_t byt[(EPL + 3) / 4];                             // row r's vector byte at bits 8 (r % 4)
+    uint32_t mym = 0;
 #pragma unroll
-    for (int i = 0; i < kOrdMaxPer; ++i) {
-      const int o = t + kOrdThreads * i;
-      if (o < M) {
-        const int v = o >> 3, k = o & 7;
-        const uint32_t below = byte[i] & ((1u << k) - 1u);
-        const int dst = (byte[i] >> k) & 1u ? re[v] - __builtin_popcount(byte[i]) + __builtin_popcount(below)
-                                            : lb[v] + k - __builtin_popcount(below);
-        arg[dst] = el[i];
-      }
+    for (int r = 0; r < EPL; ++r) {
+      if (64 * r >= M) break;
+      const int o = 64 * r + lane;
+      iv[r] = A[left + (o < M ? o : 0)];
     }
-    // children (pivot != smallest: left part; pivot != biggest: right part)
-    if (t == 0) {
-      const int pidx = misc[4];
-      const bool l_any = lt || misc[5], g_any = gt || misc[6];
-      int nsm = 0, sp2 = misc[0];
-      const int cl[2] = {L, pidx}, cr[2] = {pidx - 1, R};
-      const bool on[2] = {l_any, g_any};
-      for (int c = 0; c < 2; ++c) {
-        if (!on[c]) continue;
-        const int len = cr[c] - cl[c] + 1;
-        if (it - 1 <= 0) {
-          misc[1] = 1;                                           // std_argsort: host
-        } else if (len > 256) {
-          stk[4 * sp2] = cl[c];
-          stk[4 * sp2 + 1] = cr[c];
-          stk[4 * sp2 + 2] = it - 1;
-          ++sp2;
+#pragma unroll
+    for (int r = 0; r < EPL; ++r) {
+      if (64 * r >= M) break;
+      const bool valid = 64 * r + lane < M;
+      const double kv = K[iv[r]];
+      lt |= valid && kv < pivot;
+      gt |= valid && kv > pivot;
+      const uint64_t bm = __ballot(valid && kv >= pivot);
+      if ((lane >> 1) == r) mym = (lane & 1) ? (uint32_t)(bm >> 32) : (uint32_t)bm;
+      const uint32_t by = (uint32_t)(bm >> (lane & 56)) & 0xffu;
+      byt[r / 4] = (r % 4 ? byt[r / 4] : 0u) | (by << (8 * (r % 4)));
+    }
+    // x86-simd-sort's block schedule: blocks 1 .. nb-2 from the left or the
+    // right end, then the held-back first and last blocks
+    const int g = __builtin_popcount(mym);                   // lane b: >= pivot keys of block b
+    int lsto = left, rend = right, lp = left + 32, rp = right - 32;
+    int myl = 0, myr = 0;
+    for (int step = 0; step < nb; ++step) {
+      int b;
+      if (step < nb - 2) {
+        if (rend - rp < lp - lsto) {
+          rp -= 32;
+          b = (rp - left) >> 5;
         } else {
-          misc[8 + 2 * nsm] = cl[c];
-          misc[9 + 2 * nsm] = len;
-          ++nsm;
-          int P = 8;
-          while (P < len) P <<= 1;
-          misc[7] = max(misc[7], P);
+          b = (lp - left) >> 5;
+          lp += 32;
         }
+      } else {
+        b = step == nb - 2 ? 0 : nb - 1;
       }
-      for (int c = nsm; c < 2; ++c) misc[9 + 2 * c] = 0;
-      misc[0] = sp2;
+      if (lane == b) {
+        myl = lsto;
+        myr = rend;
+      }
+      const int gb = __builtin_amdgcn_readlane(g, b);
+      lsto += 32 - gb;
+      rend -= gb;
     }
-    __syncthreads();
+    const int pidx = lsto;
+    if (lane < nb) {
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int st = misc[8 + 2 * c], len = misc[9 + 2 * c];
-      for (int i = t; i < len; i += kOrdThreads) seg[st + i] = ((uint32_t)st << 16) | (uint32_t)len;
-    }
-    __syncthreads();
-  }
-  if (misc[1]) {
-    for (int i = t; i < n; i += kOrdThreads) perm[i] = arg[i];
-    if (t == 0) a.tiepos[shot] = -1;
-    return;
-  }
-
-  // ---- segments of <= 256 keys: argsort_n's bitonic network, all at once ----
-  const int maxP = misc[7];
-  for (int k = 2; k <= maxP; k <<= 1) {
-    for (int j = k; j >= 1; j = (j == k ? k >> 2 : j >> 1)) {  // flip(k), then half-cleaners k/4 .. 1
-      for (int p = t; p < n; p += kOrdThreads) {
-        const uint32_t info = seg[p];
-        const int len = (int)(info & 0xffffu), st = (int)(info >> 16);
-        if (len < 2) continue;
-        int P = 8;
-        while (P < len) P <<= 1;
-        if (k > P) continue;
-        const int x = p - st, y = j == k ? x ^ (k - 1) : x ^ j;
-        if (x < y && y < len) {
-          const uint16_t u = arg[st + x], w = arg[st + y];
-          if (key[w] < key[u]) {
-            arg[st + x] = w;
-            arg[st + y] = u;
-          }
-        }
+      for (int ii = 0; ii < 4; ++ii) {
+        const int c = __builtin_popcount((mym >> (8 * ii)) & 0xffu);
+        VL[4 * lane + ii] = (uint16_t)myl;
+        VR[4 * lane + ii] = (uint16_t)myr;
+        myl += 8 - c;
+        myr -= c;
       }
-      __syncthreads();
-      if (j == 1) break;
     }
+    ord_fence();
+#pragma unroll
+    for (int r = 0; r < EPL; ++r) {
+      if (64 * r >= M) break;
+      const int o = 64 * r + lane;
+      const int v = o < M ? o >> 3 : 0;
+      const int vl = VL[v], vr = VR[v];
+      if (o < M) {
+        const int kk = o & 7;
+        const uint32_t byte = (byt[r / 4] >> (8 * (r % 4))) & 0xffu;
+        const uint32_t below = byte & ((1u << kk) - 1u);
+        const int dst = (byte >> kk) & 1u ? vr - __builtin_popcount(byte) + __builtin_popcount(below)
+                                          : vl + kk - __builtin_popcount(below);
+        A[dst] = (uint16_t)iv[r];
+      }
+    }
+    ord_fence();
+    // children: pivot != smallest -> the left part, pivot != biggest -> the right part
+    const bool lany = __ballot(lt) != 0, gany = __ballot(gt) != 0;
+    if (lane == 0) {
+      if (lany) {
+        stk[3 * sp] = L;
+        stk[3 * sp + 1] = pidx - 1;
+        stk[3 * sp + 2] = it - 1;
+      }
+      if (gany) {
+        const int s2 = sp + (lany ? 1 : 0);
+        stk[3 * s2] = pidx;
+        stk[3 * s2 + 1] = R;
+        stk[3 * s2 + 2] = it - 1;
+      }
+    }
+    sp += (lany ? 1 : 0) + (gany ? 1 : 0);
+    ord_fence();
   }
-  for (int i = t; i < n; i += kOrdThreads) perm[i] = arg[i];
-  if (t == 0) a.tiepos[shot] = n;
+  for (int i = lane; i < n; i += 64) perm[i] = A[i];
+  if (lane == 0) a.tiepos[shot] = fallback ? -1 : n;
 }
 
-size_t osd_order_lds(int n) { return (size_t)14 * n + 16 + 3 * 256 * 4 + 64 * 4 + 16 * 4 + 16; }
+size_t osd_order_lds(int n) { return (size_t)10 * n + 96 * 4 + 512 * 2 + 16; }
 
 hipError_t launch_osd_order(const OrderArgs& a, long long count, hipStream_t stream) {
+  const void* k = a.n <= 256 ? (const void*)&osd_order_kernel<4>
+                : a.n <= 512 ? (const void*)&osd_order_kernel<8>
+                : a.n <= 1024 ? (const void*)&osd_order_kernel<16>
+                : (const void*)&osd_order_kernel<32>;
   long long done = 0;
   while (done < count) {
     const long long g = count - done < (1ll << 30) ? count - done : (1ll << 30);
@@ -1018,8 +1054,7 @@ hipError_t launch_osd_order(const OrderArgs& a, long long count, hipStream_t str
     ai.perm = a.perm + done * a.n;
     ai.tiepos = a.tiepos + done;
     void* params[] = {(void*)&ai};
-    hipError_t e = hipLaunchKernel((const void*)&osd_order_kernel, dim3((unsigned)g), dim3(kOrdThreads), params,
-                                   osd_order_lds(a.n), stream);
+    hipError_t e = hipLaunchKernel(k, dim3((unsigned)g), dim3(64), params, osd_order_lds(a.n), stream);
     if (e != hipSuccess) return e;
     done += g;
   }
