@@ -39,6 +39,7 @@ import hashlib
 import json
 import os
 import re
+import shlex
 import socket
 import struct
 import sys
@@ -80,6 +81,10 @@ def parse(argv=None):
                     help="N=1: also time the same workload through the HBM-resident kernel (hbm_streaming field)")
     ap.add_argument("--worklog", default=None,
                     help="write per-launch work (kernel, half-shots, iterations) as JSON (profiling)")
+    ap.add_argument("--sim-legs", default="3,4",
+                    help="end-to-end simulate_p legs after the headline, comma-separated BASELINE.json "
+                         "config indices (3: LP118_2 MS-L + OSD-0, 4: LP118_2 BP-L; p = 0.1), '' for none")
+    ap.add_argument("--sim-shots", type=int, default=1 << 20, help="shots per rank of each simulate_p leg")
     return ap.parse_args(argv)
 
 
@@ -187,12 +192,42 @@ def kernel_code_sha(path, kernel):
     return None
 
 
-def find_profile(kernel, sha, code_sha=None):
+WORKLOAD_KEYS = ("code", "algo", "schedule", "p", "iters")
+
+
+def workload_of(args):
+    """The workload a profile entry's counters depend on (not the batch size or
+    the step counts): code, decoder, schedule, channel p, iteration cap."""
+    return {k: getattr(args, k) for k in WORKLOAD_KEYS}
+
+
+def _profile_order(path):
+    """Newest first without trusting the tag's spelling: round number, then
+    the tag's letter sequence as a bijective base-26 count (r04z < r04aa),
+    then any variant suffix."""
+    tag = os.path.basename(path).split("_")[0]
+    m = re.match(r"r(\d+)([a-z]*)", tag)
+    if not m:
+        return (0, 0, tag)
+    rnd, letters = int(m.group(1)), m.group(2)
+    seq = 0
+    for ch in letters:
+        seq = seq * 26 + (ord(ch) - 96)
+    return (rnd, seq, tag)
+
+
+def find_profile(kernel, sha, code_sha=None, workload=None):
     """Newest profiles/*_roofline.json entry for this kernel built from this
     device code: the kernel's own machine-code hash (`code_sha256` of the
     entry) when both sides have it, else the whole device image's (None if the
-    committed profiles are stale for this build)."""
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_roofline.json")), reverse=True):
+    committed profiles are stale for this build). With `workload`
+    (workload_of(args)), an entry whose `bench_args` ran the same workload is
+    preferred — the per-iteration counts of one kernel differ between codes,
+    channel p and schedules; a build match of another workload is returned only
+    when no entry ran this one, flagged `workload_match: False`."""
+    other = (None, None)
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_roofline.json")), key=_profile_order, reverse=True)
+    for path in paths:
         try:
             with open(path) as f:
                 d = json.load(f)
@@ -202,11 +237,21 @@ def find_profile(kernel, sha, code_sha=None):
             if k.get("kernel") != kernel:
                 continue
             if code_sha is not None and k.get("code_sha256") is not None:
-                if k["code_sha256"] == code_sha:
-                    return os.path.relpath(path, ROOT), k
-            elif d.get("device_code_sha256") == sha:
+                if k["code_sha256"] != code_sha:
+                    continue
+            elif d.get("device_code_sha256") != sha:
+                continue
+            if workload is None:
                 return os.path.relpath(path, ROOT), k
-    return None, None
+            try:
+                ran = workload_of(parse(shlex.split(k.get("bench_args", ""))))
+            except SystemExit:
+                ran = None
+            if ran == workload:
+                return os.path.relpath(path, ROOT), dict(k, workload_match=True)
+            if other[0] is None:
+                other = (os.path.relpath(path, ROOT), dict(k, workload_match=False))
+    return other
 
 
 # ---------------------------------------------------------------------------
@@ -340,6 +385,69 @@ def cpu_baselines(args):
 
 
 # ---------------------------------------------------------------------------
+# end-to-end simulate_p legs (BASELINE.json configs[3] / configs[4])
+# ---------------------------------------------------------------------------
+SIM_LEGS = {
+    3: dict(code="LP118_2", decType="MS", decSchedule="L", OSDorder=0, decIterations=50, p=0.1,
+            config="BASELINE.json configs[3]: LP118_2, MS layered + OSD-0, 1e6 shots sharded across GPUs"),
+    4: dict(code="LP118_2", decType="BP", decSchedule="L", OSDorder=4, decIterations=100, p=0.1,
+            config="BASELINE.json configs[4]: LP118_2, BP layered + OSD order 4 (simulate never passes "
+                   "OSDorder to BP_decoder, simulator.py:281-282), p = 0.1 point of the sweep"),
+}
+
+
+def sim_leg(idx, shots_per_rank, dist=None, warmup_shots=1 << 18, sampler=None):
+    """One BASELINE config end to end through the drop-in simulate_p
+    (reference simulator.py:167-315): device sampler, decode, OSD, device
+    counters; each rank decodes its contiguous share of world x shots_per_rank
+    shots and simulate_p all-reduces the six counters (its only collective).
+    Timed between barriers + device syncs, max over ranks."""
+    from qldpcsim_amd import codes, decoders, hostcores, simulator
+    leg = SIM_LEGS[idx]
+    world = dist.get_world_size() if dist is not None else 1
+    Hx, Hz = codes.load_code(leg["code"])
+    kw = dict(decType=leg["decType"], decIterations=leg["decIterations"], decSchedule=leg["decSchedule"],
+              OSDorder=leg["OSDorder"], verbose=False, sampler=sampler)
+
+    def sync():
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+        except ImportError:
+            pass
+        if dist is not None:
+            dist.barrier()
+    if warmup_shots:
+        simulator.simulate_p(Hx, Hz, leg["p"], shots=world * min(warmup_shots, shots_per_rank), rngSeed=2, **kw)
+    decoders.reset_osd_stats()
+    sync()
+    t0 = time.perf_counter()
+    r = simulator.simulate_p(Hx, Hz, leg["p"], shots=world * shots_per_rank, rngSeed=1, **kw)
+    sync()
+    mine = time.perf_counter() - t0
+    st = dict(decoders.OSD_STATS)
+    me = {"elapsed_s": mine, "shots_per_s": shots_per_rank / mine, "host_cores": hostcores.rank_cores(),
+          "osd_shots": st["osd_shots"], "host_order_shots": st["host_order_shots"]}
+    ranks = [me]
+    if dist is not None and world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, me)
+    el = max(x["elapsed_s"] for x in ranks)
+    shots = world * shots_per_rank
+    osd = sum(x["osd_shots"] for x in ranks)
+    host = sum(x["host_order_shots"] for x in ranks)
+    return {"config": leg["config"], "code": leg["code"], "decType": leg["decType"],
+            "decSchedule": leg["decSchedule"], "OSDorder": leg["OSDorder"], "decIterations": leg["decIterations"],
+            "p": leg["p"], "shots": shots, "n_ranks": world, "value": shots / el, "unit": "shots/s",
+            "elapsed_s": el, "per_rank": ranks, "osd_shots": osd, "host_order_shots": host,
+            "host_order_share": host / osd if osd else 0.0,
+            "qBLER": 1.0 - (r["decSuccessExact"] + r["decSuccessDegen"]) / shots, "counters": r,
+            "timing": "simulate_p between barrier + device sync, max over ranks; counters all-reduced "
+                      "inside simulate_p (one all_reduce(SUM) of six int64)"}
+
+
+# ---------------------------------------------------------------------------
 # one rank
 # ---------------------------------------------------------------------------
 def run_rank(args, rank, world, local):
@@ -454,7 +562,7 @@ def run_rank(args, rank, world, local):
     algo_bytes = sum(algorithmic_bytes_per_iter(H.astype(np.int64), lp, lr, word) for H, _, lp, lr in halves) / 2
     io_bytes = 8 * ((m + 63) // 64 + (n + 63) // 64) + 4 if bits else m + n + 4
     algo_launch = algo_bytes * it_per_launch + io_bytes * hs_per_launch
-    roof = roofline(names, avg_launch_s, hs_per_launch, it_per_launch, algo_launch, launches)
+    roof = roofline(names, avg_launch_s, hs_per_launch, it_per_launch, algo_launch, launches, workload_of(args))
     try:                                   # launch geometry (older library builds lack the call)
         H0, _, lp0, lr0 = halves[0]
         w, b, lds = _lib.launch_info(H0, lp0, lr0, args.algo, dev.index)
@@ -499,6 +607,9 @@ def run_rank(args, rank, world, local):
     }
     if hbm_leg is not None:
         out["hbm_streaming"] = hbm_leg
+    legs = [int(x) for x in args.sim_legs.split(",") if x.strip()]
+    if legs and not args.worklog:
+        out["simulate"] = [sim_leg(i, args.sim_shots, dist if world > 1 else None) for i in legs]
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if rank == 0:
@@ -552,14 +663,15 @@ def hbm_streaming_leg(halves, outs, prior, args, B, bits, algo_launch, dev, step
                     "exact check node (DESIGN.md 3.6); the headline value is the LDS-resident kernel's"}
 
 
-def roofline(names, t_launch, hs_launch, it_launch, algo_launch, launches):
+def roofline(names, t_launch, hs_launch, it_launch, algo_launch, launches, workload=None):
     """The bound of the dominant decode kernel (both halves use the same kernel
-    on the bundled codes, whose Hx and Hz share a shape)."""
+    on the bundled codes, whose Hx and Hz share a shape), priced with the
+    counters of the same kernel build on the same workload."""
     from qldpcsim_amd import _lib
     kernel = names[0]
     sha = device_code_sha(_lib.LIB_PATH)
     ksha = kernel_code_sha(_lib.LIB_PATH, kernel)
-    src, prof = find_profile(kernel, sha, ksha)
+    src, prof = find_profile(kernel, sha, ksha, workload)
     r = {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
          "kernel": kernel, "kernel_ms_per_launch": t_launch * 1e3, "launches": launches,
          "units_per_launch": {"half_shots": hs_launch, "half_shot_iterations": it_launch},
@@ -573,7 +685,9 @@ def roofline(names, t_launch, hs_launch, it_launch, algo_launch, launches):
                                          "this HBM-resident kernel moves about 1.28x these bytes (post and c2v "
                                          "rows both read per edge)"),
                  "peak_gbs": HBM_PEAK_GBS},
-         "device_code_sha256": sha, "kernel_code_sha256": ksha, "profile": src}
+         "device_code_sha256": sha, "kernel_code_sha256": ksha, "profile": src,
+         "profile_bench_args": None if prof is None else prof.get("bench_args"),
+         "profile_workload_match": None if prof is None else prof.get("workload_match")}
     if prof is None:
         r["note"] = ("no counter profile under profiles/ for this kernel build "
                      "(tools/gpu_profile_roofline.sh regenerates it): bound and frac unmeasured")

@@ -357,6 +357,16 @@ def osd_policy(**kw):
         OSD_POLICY.update(old)
 
 
+# OSD shots of this process since reset_osd_stats(): every non-converged shot
+# OSD saw, and those whose reliability order the host computed (NumPy or the
+# host restatement: policy, n > 2048, or the device's NaN / fallback shots)
+OSD_STATS = {"osd_shots": 0, "host_order_shots": 0}
+
+
+def reset_osd_stats():
+    OSD_STATS.update(osd_shots=0, host_order_shots=0)
+
+
 def _host_order_only():
     return OSD_POLICY["host_order"] or not numpy_order_pinned()
 
@@ -419,6 +429,7 @@ def _osd_stage_one(H, syn, res, slot, order):
     k = int(bad.numel())
     if k == 0:
         return None
+    OSD_STATS["osd_shots"] += k
     n = res.post.shape[1]
     code = _lib.code_for(H, dev.index)
     post_b = res.post.index_select(0, bad)
@@ -561,6 +572,7 @@ def _osd_finish_device(H, syn, res, sg, hr, order):
     code = _lib.code_for(H, dev.index)
     redo, perm_h = hr
     res.osd_host_order = int(redo.size)
+    OSD_STATS["host_order_shots"] += int(redo.size)
     if redo.size:
         k2 = int(redo.size)
         idx = torch.as_tensor(redo, device=dev)
@@ -607,6 +619,8 @@ def apply_osd(H, syn, ehat, post, flags, order, nthreads=None):
     idx = np.flatnonzero((np.asarray(flags) & _lib.FLAG_CONVERGED) == 0)
     if idx.size == 0:
         return ehat
+    OSD_STATS["osd_shots"] += int(idx.size)
+    OSD_STATS["host_order_shots"] += int(idx.size)
     code = _lib.code_for(H)
     perms = np.ascontiguousarray(osd_perms(post[idx]), dtype=np.int32)
     sub_syn = np.ascontiguousarray(syn[idx], dtype=np.uint8)

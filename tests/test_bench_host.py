@@ -77,3 +77,32 @@ def test_no_device_fails_loudly():
     r = subprocess.run([sys.executable, "bench.py", "--cpu-seconds", "0"], cwd=ROOT, capture_output=True,
                        text=True, timeout=120)
     assert r.returncode != 0 and "no HIP device" in r.stderr
+
+
+def test_find_profile_matches_the_workload(tmp_path, monkeypatch):
+    """Two entries of one kernel build (same machine-code hash) profiled on
+    different workloads: the roofline takes the counters of its own workload
+    (code, decoder, schedule, p, iterations), newest round first whatever the
+    tag spelling (r04z < r04aa), and flags a build match of another workload."""
+    import json
+    d = tmp_path / "profiles"
+    d.mkdir()
+    ent = lambda args, v: {"kernel": "ms_layered_kernel<8, 1>", "code_sha256": "ab" * 32,  # noqa: E731
+                           "bench_args": args, "per_half_shot_iteration": {"valu_insts": v}}
+    (d / "r04z_roofline.json").write_text(json.dumps({"kernels": [
+        ent("--code LP118_2 --schedule L --p 0.1 --batch 131072", 3.0)]}))
+    (d / "r04aa_roofline.json").write_text(json.dumps({"kernels": [
+        ent("--code LP118_2 --schedule L --p 0.05 --batch 262144", 1.0),
+        ent("--code LP118_2 --schedule L --p 0.1 --batch 131072", 2.0)]}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    w = bench.workload_of(bench.parse(["--code", "LP118_2", "--schedule", "L", "--p", "0.1"]))
+    src, k = bench.find_profile("ms_layered_kernel<8, 1>", None, "ab" * 32, w)
+    assert src.endswith("r04aa_roofline.json") and k["per_half_shot_iteration"]["valu_insts"] == 2.0
+    assert k["workload_match"] is True
+    w5 = bench.workload_of(bench.parse(["--code", "LP118_2", "--schedule", "L", "--p", "0.05"]))
+    assert bench.find_profile("ms_layered_kernel<8, 1>", None, "ab" * 32, w5)[1]["per_half_shot_iteration"] == \
+        {"valu_insts": 1.0}
+    wf = bench.workload_of(bench.parse(["--code", "LP118_0"]))
+    src, k = bench.find_profile("ms_layered_kernel<8, 1>", None, "ab" * 32, wf)
+    assert k["workload_match"] is False
+    assert bench.find_profile("ms_layered_kernel<8, 1>", None, "cd" * 32, w) == (None, None)

@@ -63,3 +63,40 @@ def test_two_rank_gloo_counters_equal_single_process():
     mp.spawn(_worker, args=(2, _free_port(), shots, out), nprocs=2, join=True)
     assert out[0] == single and out[1] == single
     assert single["decSuccessExact"] > 0 and single["Avg_number_of_iterations_X"] > 1.0
+
+
+def _oracle_decode_batch_osd(H, syndromes, p, max_iter, layers=None, algo="MS", beta=0.75, eps=1e-9,
+                             want_post=False, osd_order=-1, layer_ptr=None, layer_rows=None, stream=None):
+    from qldpcsim_amd import decoders
+    r = _oracle_decode_batch(H, syndromes, p, max_iter, layers, algo, beta, eps, True, -1, layer_ptr, layer_rows)
+    if osd_order >= 0:
+        decoders.apply_osd(H, syndromes, r.ehat, r.post, r.flags, osd_order, nthreads=1)
+    return r
+
+
+def _bench_leg_worker(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from qldpcsim_amd import decoders
+    decoders.decode_batch = _oracle_decode_batch_osd
+    out[rank] = bench.sim_leg(3, 24, dist, warmup_shots=0, sampler="host")
+    dist.destroy_process_group()
+
+
+def test_bench_simulate_leg_two_ranks_gloo():
+    """bench.py's end-to-end configs[3] leg under two gloo ranks (the decode
+    replaced by the CPU oracle + host OSD here): both ranks report the same
+    all-reduced counters over both shares, per-rank rates and host cores, and
+    the OSD shots' host-order share (all of them on this host path)."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_bench_leg_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    a, b = out[0], out[1]
+    assert a["counters"] == b["counters"] and a["shots"] == b["shots"] == 48 and a["n_ranks"] == 2
+    c = a["counters"]
+    assert c["decSuccessExact"] + c["decSuccessDegen"] <= 48 and a["value"] > 0
+    assert len(a["per_rank"]) == 2 and all(r["host_cores"] >= 1 and r["shots_per_s"] > 0 for r in a["per_rank"])
+    assert a["osd_shots"] == sum(r["osd_shots"] for r in a["per_rank"]) > 0
+    assert a["host_order_share"] == 1.0

@@ -31,9 +31,14 @@ def _bench(*args, env=None, timeout=110):
 
 
 def test_bench_single_gpu_line():
-    r = _bench("--steps", "2", "--warmup", "1", "--batch", "65536", "--cpu-seconds", "1")
+    r = _bench("--steps", "2", "--warmup", "1", "--batch", "65536", "--cpu-seconds", "1", "--sim-shots", "65536")
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
+    sim = {x["decType"]: x for x in d["simulate"]}            # the configs[3] / configs[4] legs
+    assert set(sim) == {"MS", "BP"} and all(x["shots"] == 65536 and x["value"] > 0 for x in sim.values())
+    assert sim["MS"]["osd_shots"] > 0 and sim["MS"]["host_order_shots"] == 0   # NumPy's order on the device
+    assert sim["BP"]["osd_shots"] == 0                         # simulate never passes OSDorder to BP
+    assert 0.5 < sim["MS"]["qBLER"] < 1.0
     assert KEYS <= set(d) and d["n_gpus"] == 1 and d["value"] > 0
     rf = d["roofline"]
     assert rf["kernel"] == "ms_flood_kernel<8, 4>"
@@ -56,7 +61,8 @@ def test_bench_hbm_path_line():
     """--path hbm times the HBM-resident kernel as the main leg: same workload,
     its roofline includes the measured-HBM unit (bound hbm when the committed
     profile matches this build)."""
-    r = _bench("--path", "hbm", "--steps", "1", "--warmup", "1", "--batch", "65536", "--cpu-seconds", "0")
+    r = _bench("--path", "hbm", "--steps", "1", "--warmup", "1", "--batch", "65536", "--cpu-seconds", "0",
+               "--sim-legs", "")
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
     rf = d["roofline"]
@@ -69,7 +75,7 @@ def test_bench_hbm_path_line():
 
 def test_bench_layered_channel_line():
     r = _bench("--steps", "1", "--warmup", "1", "--batch", "16384", "--cpu-seconds", "0",
-               "--code", "LP118_2", "--schedule", "L", "--p", "0.05")
+               "--code", "LP118_2", "--schedule", "L", "--p", "0.05", "--sim-legs", "")
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
     assert d["roofline"]["kernel"].startswith("ms_layered_kernel<8")
@@ -79,11 +85,16 @@ def test_bench_layered_channel_line():
 def test_bench_spawns_ranks_itself_over_gloo():
     env = dict(os.environ, QLDPC_BENCH_BACKEND="gloo")
     env.pop("WORLD_SIZE", None)
-    r = _bench("--gpus", "2", "--steps", "1", "--warmup", "1", "--batch", "16384", env=env)
+    r = _bench("--gpus", "2", "--steps", "1", "--warmup", "1", "--batch", "16384", "--sim-legs", "3",
+               "--sim-shots", "32768", env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * 16384
     assert "cpu_baseline" not in d and d["value"] > 0
+    leg, = d["simulate"]                                      # configs[3], each rank its share, one all-reduce
+    assert leg["n_ranks"] == 2 and leg["shots"] == 2 * 32768 and len(leg["per_rank"]) == 2
+    c = leg["counters"]
+    assert 0 < c["decSuccessExact"] + c["decSuccessDegen"] < leg["shots"] and leg["host_order_shots"] == 0
 
 
 def test_bench_refuses_more_ranks_than_gpus_over_rccl():
@@ -92,7 +103,7 @@ def test_bench_refuses_more_ranks_than_gpus_over_rccl():
     env.pop("WORLD_SIZE", None)
     import torch
     n = torch.cuda.device_count()
-    r = _bench("--gpus", str(n + 1), "--steps", "1", "--warmup", "0", "--batch", "1024", env=env)
+    r = _bench("--gpus", str(n + 1), "--steps", "1", "--warmup", "0", "--batch", "1024", "--sim-legs", "", env=env)
     assert r.returncode != 0 and "HIP device(s) visible" in r.stderr
 
 
@@ -100,7 +111,8 @@ def test_bench_two_ranks_share_gpu_over_gloo_torchrun():
     env = dict(os.environ, QLDPC_BENCH_BACKEND="gloo")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", "29531", "bench.py", "--gpus", "2",
-                        "--steps", "1", "--warmup", "1", "--batch", "16384"],
+                        "--steps", "1", "--warmup", "1", "--batch", "16384", "--sim-legs", "3", "--sim-shots",
+                        "16384"],
                        cwd=ROOT, capture_output=True, text=True, timeout=110, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
