@@ -161,7 +161,8 @@ int qldpc_osd_decode(const qldpc_code *code, const uint8_t *h_syn, const int32_t
                      uint8_t *h_ehat, int32_t *h_J, int32_t *h_J_size, int first_info_index);
 
 /* Batched OSD over `count` shots (syn uint8[count][m], perm int32[count][n],
- * ehat uint8[count][n] in/out), `nthreads` host threads (<=0: hardware). */
+ * ehat uint8[count][n] in/out), `nthreads` host threads (<= 0: the process's
+ * budget — affinity mask, cgroup cpu.max quota, OMP_NUM_THREADS). */
 int qldpc_osd_decode_batch(const qldpc_code *code, int64_t count, const uint8_t *h_syn,
                            const int32_t *h_perm, int order, uint8_t *h_ehat, int nthreads);
 
@@ -188,7 +189,8 @@ int qldpc_osd_device(const qldpc_code *code, int64_t count, const uint8_t *d_syn
 int qldpc_osd_order_device(const qldpc_code *code, int64_t count, const double *d_post, int32_t *d_perm,
                            int32_t *d_tiepos, void *stream);
 
-/* The same order on the host (C++, `nthreads` threads): h_perm int32[count][n],
+/* The same order on the host (C++, `nthreads` threads, <= 0: the process's
+ * budget as qldpc_osd_decode_batch): h_perm int32[count][n],
  * h_status int32[count] = 0 exact, 1 left to NumPy (as tiepos -1 above).
  * Used to check at import that the running NumPy dispatches to the restated
  * functions (qldpcsim_amd/decoders.py), and by the host OSD path. */

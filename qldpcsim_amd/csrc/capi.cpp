@@ -703,15 +703,17 @@ static void team_layout(const qldpc_code* c, int w, int* bytes, int* off_c2v, in
   *bytes = off;
 }
 
-static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
+// The launch configuration of (schedule, algo), copied into *out under the
+// schedule's lock: a launch keeps its own consistent snapshot even if an
+// option change (qldpc_set_option) rebuilds the cached one meanwhile.
+static int launch_config(qldpc_schedule* s, int algo, LaunchCfg* out) {
   std::lock_guard<std::mutex> lk(s->mu);
-  LaunchCfg& cfg = s->cfg[algo];
   const uint32_t gen = g_opt.gen.load();
-  if (cfg.ok && cfg.gen == gen) {
-    *out = &cfg;
+  if (s->cfg[algo].ok && s->cfg[algo].gen == gen) {
+    *out = s->cfg[algo];
     return QLDPC_OK;
   }
-  cfg = LaunchCfg{};
+  LaunchCfg cfg{};                                   // built aside, published whole
   const qldpc_code* c = s->code;
   const int dc = fast_table_ok(c) ? c->uniform_deg : 0;
   cfg.kernel = nullptr;
@@ -823,7 +825,8 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg** out) {
   cfg.hbm = best_waves == 0;
   cfg.ok = true;
   cfg.gen = gen;
-  *out = &cfg;
+  s->cfg[algo] = cfg;
+  *out = cfg;
   return QLDPC_OK;
 }
 
@@ -879,13 +882,13 @@ extern "C" int qldpc_timing_read(double* total_ms, int64_t* launches) {
 // their tables and per-half-shot state fit, else the HBM-resident kernel
 // (hbm_kernels.hip). Option force_hbm takes the HBM kernel for any code
 // (tests: the two families agree bit for bit).
-static int choose_path(qldpc_schedule* s, int algo, LaunchCfg** cfg, bool* hbm) {
+static int choose_path(qldpc_schedule* s, int algo, LaunchCfg* cfg, bool* hbm) {
   const qldpc_code* c = s->code;
   *hbm = !s->lds_ok || opt(&Options::force_hbm) != 0 || (algo == QLDPC_ALGO_MS && c->max_row_deg > 32) ||
          (algo == QLDPC_ALGO_BP && c->max_col_deg > 128);
   if (*hbm) return QLDPC_OK;
   const int rc = launch_config(s, algo, cfg);
-  if (rc == QLDPC_OK && (*cfg)->hbm) *hbm = true;   // LDS image / state does not fit a CU
+  if (rc == QLDPC_OK && cfg->hbm) *hbm = true;      // LDS image / state does not fit a CU
   return rc;
 }
 
@@ -1030,9 +1033,10 @@ extern "C" int qldpc_decode_device_ex(const qldpc_code* code, const qldpc_schedu
   int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
   if (dev != code->device) return fail(QLDPC_EINVAL, "code lives on device %d, current device is %d", code->device, dev);
-  LaunchCfg* cfg = nullptr;
+  LaunchCfg cfgv;
+  LaunchCfg* cfg = &cfgv;
   bool hbm = false;
-  int rc = choose_path(sched, algo, &cfg, &hbm);
+  int rc = choose_path(sched, algo, cfg, &hbm);
   if (rc) return rc;
   if (hbm)
     return decode_hbm(code, sched, algo, d_syn, syn_format, batch, p, max_iter, beta, eps, d_ehat, ehat_format,
@@ -1154,9 +1158,10 @@ extern "C" int qldpc_decode_kernel_name(const qldpc_code* code, const qldpc_sche
   if (!code || !sched || !buf || len <= 0) return fail(QLDPC_EINVAL, "null argument");
   if (algo != QLDPC_ALGO_MS && algo != QLDPC_ALGO_BP) return fail(QLDPC_EINVAL, "Unrecognized decoder type.");
   if (code->device < 0 || !sched->d_blob) return fail(QLDPC_EHIP, "no HIP device was visible when the code/schedule was created");
-  LaunchCfg* cfg = nullptr;
+  LaunchCfg cfgv;
+  LaunchCfg* cfg = &cfgv;
   bool hbm = false;
-  int rc = choose_path(sched, algo, &cfg, &hbm);
+  int rc = choose_path(sched, algo, cfg, &hbm);
   if (rc) return rc;
   const char* hname = nullptr;
   if (hbm) (void)qldpc::select_hbm_kernel(algo, code->max_row_deg, &hname);
@@ -1170,9 +1175,10 @@ extern "C" int qldpc_decode_launch_info(const qldpc_code* code, const qldpc_sche
   if (!code || !sched || !waves_per_wg || !wg_per_cu || !lds_bytes) return fail(QLDPC_EINVAL, "null argument");
   if (algo != QLDPC_ALGO_MS && algo != QLDPC_ALGO_BP) return fail(QLDPC_EINVAL, "Unrecognized decoder type.");
   if (code->device < 0 || !sched->d_blob) return fail(QLDPC_EHIP, "no HIP device was visible when the code/schedule was created");
-  LaunchCfg* cfg = nullptr;
+  LaunchCfg cfgv;
+  LaunchCfg* cfg = &cfgv;
   bool hbm = false;
-  int rc = choose_path(sched, algo, &cfg, &hbm);
+  int rc = choose_path(sched, algo, cfg, &hbm);
   if (rc) return rc;
   *waves_per_wg = hbm ? 0 : cfg->waves;
   *wg_per_cu = hbm ? 0 : cfg->blocks_per_cu;
@@ -1465,11 +1471,13 @@ extern "C" int qldpc_osd_decode(const qldpc_code* code, const uint8_t* h_syn, co
   return osd_one(code, h_syn, h_perm, order, h_ehat, h_J, h_J_size, first_info_index);
 }
 
+int qldpc_host_thread_budget();                         // np_order.cpp
+
 extern "C" int qldpc_osd_decode_batch(const qldpc_code* code, int64_t count, const uint8_t* h_syn,
                                       const int32_t* h_perm, int order, uint8_t* h_ehat, int nthreads) {
   if (!code) return fail(QLDPC_EINVAL, "code is null");
   if (count <= 0) return QLDPC_OK;
-  if (nthreads <= 0) nthreads = (int)std::max(1u, std::thread::hardware_concurrency());
+  if (nthreads <= 0) nthreads = qldpc_host_thread_budget();
   nthreads = (int)std::min<int64_t>(nthreads, count);
   const int m = code->m, n = code->n;
   std::atomic<int64_t> next{0};

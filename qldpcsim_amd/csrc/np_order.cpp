@@ -37,6 +37,9 @@
 
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <sched.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -147,6 +150,30 @@ struct NpOrder {
 
 }  // namespace
 
+// Host threads this process may use (qldpcsim_amd/hostcores.py's
+// process_cores): the affinity mask, capped by the cgroup CPU quota
+// (cpu.max) and by OMP_NUM_THREADS — not hardware_concurrency(), which counts
+// CPUs the process may not run on.
+int qldpc_host_thread_budget() {
+  int n = (int)std::max(1u, std::thread::hardware_concurrency());
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) n = std::max(1, CPU_COUNT(&set));
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[64] = {0};
+    double per = 0;
+    if (fscanf(f, "%63s %lf", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0)
+      n = std::min(n, std::max(1, (int)(atof(q) / per)));
+    fclose(f);
+  }
+  if (const char* e = getenv("OMP_NUM_THREADS")) {
+    const int o = atoi(e);
+    if (o > 0) n = std::min(n, o);
+  }
+  return n;
+}
+
+
 // One row: keys from the posteriors, NumPy's argsort. 0 = exact, 1 = a case
 // this restatement leaves to NumPy (a NaN key, or x86-simd-sort's std::sort
 // fallback after 2 floor(log2 n) levels).
@@ -171,7 +198,7 @@ extern "C" int qldpc_osd_order_host(const double* h_post, int64_t count, int n, 
   if (count < 0 || n < 0) return QLDPC_EINVAL;
   if (count == 0 || n == 0) return QLDPC_OK;
   if (!h_post || !h_perm || !h_status) return QLDPC_EINVAL;
-  if (nthreads <= 0) nthreads = 1;
+  if (nthreads <= 0) nthreads = qldpc_host_thread_budget();
   nthreads = (int)std::min<int64_t>(nthreads, count);
   std::atomic<int64_t> next{0};
   auto worker = [&]() {

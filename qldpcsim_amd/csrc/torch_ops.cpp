@@ -15,8 +15,9 @@
 // [B, ceil(m/64)] (bit-packed words) on a HIP device; H [m, n] and the
 // schedule (layer_ptr [L+1], layer_rows, int32 or int64) as CPU tensors.
 // The cache is keyed by a 128-bit hash of H's own bytes (dtype and shape
-// included), so a call with a cached H reads it once and copies nothing;
-// torch.ops.qldpc.release() synchronizes the devices and frees the cache.
+// included) and a hit is confirmed against the stored bytes, so a call with a
+// cached H reads it twice and copies nothing; torch.ops.qldpc.release()
+// waits for calls in flight, synchronizes the devices and frees the cache.
 // Errors as decode_batch / the reference: ValueError for shapes / options
 // (and for CPU syndromes: there is no CPU path), IndexError for layer rows out
 // of range (decoders.py:156, :250), RuntimeError for HIP failures.
@@ -28,6 +29,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <tuple>
 #include <utility>
@@ -38,10 +40,12 @@
 namespace {
 
 struct CodeEntry {
+  std::vector<unsigned char> bytes;                          // H's own bytes (confirms a hash hit)
   qldpc_code* code = nullptr;
   std::map<std::vector<int32_t>, qldpc_schedule*> scheds;   // key: layer_ptr ++ layer_rows
 };
-std::mutex g_mu;
+std::mutex g_mu;           // the cache map
+std::shared_mutex g_live;  // decodes in flight (shared) vs release() (exclusive)
 struct CodeKey {
   int dev;
   int64_t m, n;
@@ -51,7 +55,7 @@ struct CodeKey {
     return std::tie(dev, m, n, dtype, h0, h1) < std::tie(o.dev, o.m, o.n, o.dtype, o.h0, o.h1);
   }
 };
-std::map<CodeKey, CodeEntry> g_codes;
+std::map<CodeKey, std::vector<CodeEntry>> g_codes;   // entries with equal hashes: distinct bytes
 
 // four-lane multiply-rotate hash (xxh64's round) over the bytes: ~10 GB/s,
 // so a cached H costs one read instead of a mod-2 copy into a string key
@@ -120,13 +124,24 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> decode_hip(
   skey.insert(skey.end(), lr.begin(), lr.end());
   qldpc_code* code = nullptr;
   qldpc_schedule* sched = nullptr;
+  // held until the launch is queued: release() cannot free the code or the
+  // schedule this call uses
+  std::shared_lock<std::shared_mutex> live(g_live);
   {
     std::lock_guard<std::mutex> lk(g_mu);
-    CodeEntry& ce = g_codes[key];
-    if (!ce.code) {
+    std::vector<CodeEntry>& cands = g_codes[key];
+    CodeEntry* hit = nullptr;
+    for (CodeEntry& c : cands)
+      if (c.bytes.size() == hbytes && memcmp(c.bytes.data(), hp, hbytes) == 0) hit = &c;
+    if (!hit) {                                               // new H (or a hash collision)
+      CodeEntry ne;
+      ne.bytes.assign(hp, hp + hbytes);
       const at::Tensor Hb = Hc.remainder(2).to(at::kByte).contiguous();     // load_matrix's (mat % 2)
-      check(qldpc_code_create(Hb.data_ptr<uint8_t>(), (int)m, (int)n, &ce.code));
+      check(qldpc_code_create(Hb.data_ptr<uint8_t>(), (int)m, (int)n, &ne.code));
+      cands.push_back(std::move(ne));
+      hit = &cands.back();
     }
+    CodeEntry& ce = *hit;
     code = ce.code;
     auto it = ce.scheds.find(skey);
     if (it == ce.scheds.end()) {
@@ -162,12 +177,15 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> decode_cpu(
 // Frees every cached graph and schedule (their device tables and HBM
 // workspaces) after the devices holding them have finished all work.
 void release() {
+  std::unique_lock<std::shared_mutex> live(g_live);          // no decode call in flight
   std::lock_guard<std::mutex> lk(g_mu);
   for (auto& kv : g_codes) {
     const c10::hip::HIPGuardMasqueradingAsCUDA guard(c10::Device(c10::DeviceType::CUDA, kv.first.dev));
     TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "qldpc::release: device synchronize failed");
-    for (auto& s : kv.second.scheds) qldpc_schedule_destroy(s.second);
-    qldpc_code_destroy(kv.second.code);
+    for (auto& ce : kv.second) {
+      for (auto& s : ce.scheds) qldpc_schedule_destroy(s.second);
+      qldpc_code_destroy(ce.code);
+    }
   }
   g_codes.clear();
 }

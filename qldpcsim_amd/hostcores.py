@@ -2,9 +2,10 @@
 capped by a cgroup CPU quota and by OMP_NUM_THREADS), shared by the ranks of
 one node (LOCAL_WORLD_SIZE under torch.distributed.run). The host side of the
 simulator's shot loop (simulator.py:244-315 in the reference) — NumPy's
-reliability order for the OSD shots the device order cannot certify, and the
-host C++ OSD — sizes its thread pools from this, so 8 ranks on one node do
-not each start a pool the size of the whole machine."""
+reliability order for the rare OSD shots the device order leaves to NumPy,
+the host order and the host C++ OSD — sizes its thread pools from this, so 8
+ranks on one node do not each start a pool the size of the whole machine.
+The library's C++ default (nthreads <= 0) computes the same process budget."""
 import os
 
 
@@ -30,12 +31,23 @@ def process_cores():
     return n, " capped by ".join(how)
 
 
+def _pinned():
+    """Whether this process is pinned to a strict subset of the machine's CPUs
+    (a launcher that gives each rank its own CPU set)."""
+    try:
+        return len(os.sched_getaffinity(0)) < (os.cpu_count() or 1)
+    except AttributeError:
+        return False
+
+
 def rank_cores(cap=16):
-    """Host threads one rank should use: the process budget divided among the
-    node's ranks (LOCAL_WORLD_SIZE; ranks started without it share the
-    affinity mask with nobody we know of), at most `cap`, at least 1."""
+    """Host threads one rank should use, at most `cap`, at least 1: a rank
+    pinned to its own CPU set uses that set (already its share); otherwise the
+    process budget is the node's, divided among its ranks (LOCAL_WORLD_SIZE;
+    ranks started without it share the machine with nobody we know of)."""
     cores, _ = process_cores()
+    if _pinned():
+        return max(1, min(cap, cores))
     local = os.environ.get("LOCAL_WORLD_SIZE", "1")
     share = max(1, int(local)) if local.isdigit() else 1
-    # ranks pinned to disjoint CPU sets already see only their own share
     return max(1, min(cap, cores // share if cores >= share else 1))

@@ -45,8 +45,13 @@ def test_library_options_roundtrip_and_unknown_names():
     assert _lib.get_option("force_hbm") == 0 and _lib.get_option("bp_team_w") == 0
     with pytest.raises(ValueError, match="unknown option"):
         _lib.set_option("no_such_option", 1)
-    src = open(os.path.join(ROOT, "qldpcsim_amd", "csrc", "capi.cpp")).read()
-    assert "getenv" not in src
+    import glob
+    import re
+    for f in glob.glob(os.path.join(ROOT, "qldpcsim_amd", "csrc", "*.cpp")):
+        # options never come from the environment; the one variable read is
+        # the host thread budget's OMP_NUM_THREADS (hostcores.py's convention)
+        calls = re.findall(r"getenv\(([^)]*)\)", open(f).read())
+        assert set(calls) <= {'"OMP_NUM_THREADS"'}, (f, calls)
 
 
 def test_version_and_device_count():

@@ -239,3 +239,21 @@ def test_large_codes_use_the_host_sampler():
     from qldpcsim_amd import simulator
     assert simulator._channel_ok(np.zeros((3, 4096)), np.zeros((3, 4096)))
     assert not simulator._channel_ok(np.zeros((3, 4097)), np.zeros((3, 4097)))
+
+
+def test_rank_cores_pinned_vs_shared(monkeypatch):
+    """hostcores.rank_cores: a rank pinned to its own CPU set uses that set;
+    an unpinned rank divides the machine's budget among the node's ranks."""
+    import os
+    from qldpcsim_amd import hostcores
+    monkeypatch.delenv("OMP_NUM_THREADS", raising=False)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    monkeypatch.setattr(os, "cpu_count", lambda: 128)
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(16)))         # pinned: 16 of 128
+    monkeypatch.setattr(hostcores, "process_cores", lambda: (16, "sched_getaffinity"))
+    assert hostcores.rank_cores() == 16
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(128)))        # whole machine, shared
+    monkeypatch.setattr(hostcores, "process_cores", lambda: (128, "sched_getaffinity"))
+    assert hostcores.rank_cores() == 16 and hostcores.rank_cores(cap=64) == 16
+    monkeypatch.setattr(hostcores, "process_cores", lambda: (64, "cgroup cpu.max"))
+    assert hostcores.rank_cores() == 8
