@@ -760,83 +760,94 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
 // ---------------------------------------------------------------------------
 __constant__ double kExpHL[32] = QLDPC_EXP_HL_INIT;
 
+// A key and its index travel as one 64-bit word: w = u << 11 | i, u =
+// bits(key) - bits(0.5) (key in [0.5, 1]: u <= 2^52, order-preserving), i < 2048.
+// Comparisons look at the key part only — equal keys compare equal whatever
+// their indices, exactly as x86-simd-sort compares the float64 keys:
+//   key(b) < key(a)  <=>  (b | 0x7ff) < (a & ~0x7ff)
+constexpr uint64_t kOrdIdx = 0x7ffull;
+__device__ __forceinline__ bool ord_less(uint64_t b, uint64_t a) { return (b | kOrdIdx) < (a & ~kOrdIdx); }
+
 // compare-exchange of two registers of one lane (positions lo < hi)
-__device__ __forceinline__ void ord_cx(double& klo, int& ilo, double& khi, int& ihi) {
-  const bool sw = khi < klo;
-  const double k = klo;
-  const int i = ilo;
-  klo = sw ? khi : klo;
-  ilo = sw ? ihi : ilo;
-  khi = sw ? k : khi;
-  ihi = sw ? i : ihi;
+__device__ __forceinline__ void ord_cx(uint64_t& lo, uint64_t& hi) {
+  const bool sw = ord_less(hi, lo);
+  const uint64_t t = lo;
+  lo = sw ? hi : lo;
+  hi = sw ? t : hi;
 }
 
-// within-lane stage: partner position x ^ m, m in {1, 2, 3}
-__device__ __forceinline__ void ord_within(double (&k)[4], int (&id)[4], int m) {
-  if (m == 1) {
-    ord_cx(k[0], id[0], k[1], id[1]);
-    ord_cx(k[2], id[2], k[3], id[3]);
-  } else if (m == 2) {
-    ord_cx(k[0], id[0], k[2], id[2]);
-    ord_cx(k[1], id[1], k[3], id[3]);
+// within-lane stage: partner position x ^ M, M in {1, 2, 3}. Every stage is
+// a compile-time instance: with the partner pattern a run-time value, the
+// compiler kept the four words in scratch memory and addressed them by it.
+template <int M>
+__device__ __forceinline__ void ord_within(uint64_t (&w)[4]) {
+  if constexpr (M == 1) {
+    ord_cx(w[0], w[1]);
+    ord_cx(w[2], w[3]);
+  } else if constexpr (M == 2) {
+    ord_cx(w[0], w[2]);
+    ord_cx(w[1], w[3]);
   } else {
-    ord_cx(k[0], id[0], k[3], id[3]);
-    ord_cx(k[1], id[1], k[2], id[2]);
+    ord_cx(w[0], w[3]);
+    ord_cx(w[1], w[2]);
   }
 }
 
-// cross-lane stage: partner position x ^ m, m >= 4: lane ^ lm (lm = m >> 2),
-// register r ^ M3 (M3 = m & 3); hb = the highest bit of lm decides which side
+// cross-lane stage: partner position x ^ m, m >= 4: lane ^ LM (LM = m >> 2),
+// register r ^ M3 (M3 = m & 3); HB = the highest bit of LM decides which side
 // is the lower position
-template <int M3>
-__device__ __forceinline__ void ord_cross(double (&k)[4], int (&id)[4], int lm, int hb, int lane) {
-  const bool lo = (lane & hb) == 0;
-  double nk[4];
-  int ni[4];
+template <int LM, int HB, int M3>
+__device__ __forceinline__ void ord_cross(uint64_t (&w)[4], int lane) {
+  const bool lo = (lane & HB) == 0;
+  uint64_t nw[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const double pk = __shfl_xor(k[r ^ M3], lm, 64);
-    const int pi = __shfl_xor(id[r ^ M3], lm, 64);
-    const bool take = lo ? pk < k[r] : k[r] < pk;
-    nk[r] = take ? pk : k[r];
-    ni[r] = take ? pi : id[r];
+    const uint64_t pw = __shfl_xor(w[r ^ M3], LM, 64);
+    const bool take = lo ? ord_less(pw, w[r]) : ord_less(w[r], pw);
+    nw[r] = take ? pw : w[r];
   }
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    k[r] = nk[r];
-    id[r] = ni[r];
-  }
+  for (int r = 0; r < 4; ++r) w[r] = nw[r];
 }
 
-// argsort_n on positions [L, L + N), N <= 256, in registers (K: keys by
-// original index, A: the arrangement)
-__device__ __forceinline__ void ord_small(const double* K, uint16_t* A, int L, int N, int lane) {
-  int P = 8;
-  while (P < N) P <<= 1;
-  double k[4];
-  int id[4];
+// half-cleaners J, J/2 .. 1
+template <int J>
+__device__ __forceinline__ void ord_half(uint64_t (&w)[4], int lane) {
+  if constexpr (J >= 4) ord_cross<J / 4, J / 4, 0>(w, lane);
+  else if constexpr (J >= 1) ord_within<J>(w);
+  if constexpr (J > 1) ord_half<J / 2>(w, lane);
+}
+
+// bitonic merge of blocks of KK: flip(KK), then half-cleaners KK/4 .. 1
+template <int KK>
+__device__ __forceinline__ void ord_merge(uint64_t (&w)[4], int lane) {
+  if constexpr (KK <= 4) ord_within<KK - 1>(w);              // flip(2) = x ^ 1, flip(4) = x ^ 3
+  else ord_cross<(KK - 1) / 4, KK / 8, 3>(w, lane);          // flip(KK) = x ^ (KK - 1)
+  if constexpr (KK >= 4) ord_half<KK / 4>(w, lane);
+}
+
+// argsort_n on positions [L, L + N), N <= 256, in registers
+__device__ __forceinline__ void ord_small(uint64_t* W, int L, int N, int lane) {
+  uint64_t w[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int x = 4 * lane + r;
-    id[r] = A[L + (x < N ? x : 0)];
+    const uint64_t v = W[L + (x < N ? x : 0)];
+    w[r] = x < N ? v : ~0ull;                               // +inf pads
   }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const double v = K[id[r]];
-    k[r] = 4 * lane + r < N ? v : __builtin_inf();
-  }
-  for (int kk = 2; kk <= P; kk <<= 1) {
-    if (kk <= 4) ord_within(k, id, kk - 1);                   // flip(2) = x ^ 1, flip(4) = x ^ 3
-    else ord_cross<3>(k, id, (kk - 1) >> 2, kk >> 3, lane);   // flip(kk) = x ^ (kk - 1)
-    for (int j = kk >> 2; j >= 1; j >>= 1) {                  // half-cleaners kk/4 .. 1
-      if (j >= 4) ord_cross<0>(k, id, j >> 2, j >> 2, lane);
-      else ord_within(k, id, j);
-    }
-  }
+  // stages up to P = max(8, 2^ceil(log2 N)) (uniform branches)
+  ord_merge<2>(w, lane);
+  ord_merge<4>(w, lane);
+  ord_merge<8>(w, lane);
+  if (N > 8) ord_merge<16>(w, lane);
+  if (N > 16) ord_merge<32>(w, lane);
+  if (N > 32) ord_merge<64>(w, lane);
+  if (N > 64) ord_merge<128>(w, lane);
+  if (N > 128) ord_merge<256>(w, lane);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int x = 4 * lane + r;
-    if (x < N) A[L + x] = (uint16_t)id[r];
+    if (x < N) W[L + x] = w[r];
   }
 }
 
@@ -849,11 +860,10 @@ template <int EPL>                                          // keys per lane cap
 __global__ void __launch_bounds__(64) osd_order_kernel(OrderArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int n = a.n;
-  double* K = (double*)lds;                                  // [n] keys by original index
-  int* stk = (int*)(K + n);                                  // [32][3] (L, R, iters)
+  uint64_t* W = (uint64_t*)lds;                              // [n] (key, index) words, current arrangement
+  int* stk = (int*)(W + n);                                  // [32][3] (L, R, iters)
   uint16_t* VL = (uint16_t*)(stk + 96);                      // [256] per vector: lt store base
   uint16_t* VR = VL + 256;                                   // [256] per vector: ge store end
-  uint16_t* A = VR + 256;                                    // [n] the arrangement (indices)
   const int lane = threadIdx.x;
   const long long shot = blockIdx.x;
   const double* post = a.post + shot * (long long)n;
@@ -863,8 +873,7 @@ __global__ void __launch_bounds__(64) osd_order_kernel(OrderArgs a) {
   for (int i = lane; i < n; i += 64) {
     const double k = qldpc_osd_key_t(post[i], kExpHL);
     nan |= k != k;
-    K[i] = k;
-    A[i] = (uint16_t)i;
+    W[i] = ((__builtin_bit_cast(uint64_t, k) - 0x3FE0000000000000ull) << 11) | (uint64_t)i;
   }
   bool fallback = __ballot(nan) != 0;                        // std_argsort_withnan: the host's
   int lg = 0;
@@ -889,24 +898,28 @@ __global__ void __launch_bounds__(64) osd_order_kernel(OrderArgs a) {
       break;
     }
     if (R + 1 - L <= 256) {
-      ord_small(K, A, L, R + 1 - L, lane);
+      if constexpr ((QLDPC_ABLATE_ORD & 1) == 0) ord_small(W, L, R + 1 - L, lane);
       ord_fence();
       continue;
     }
+    if constexpr ((QLDPC_ABLATE_ORD & 2) != 0) continue;
     // ---- argpartition_unrolled<4> ----
+    // pivot: the 5th smallest key of the 8 samples (every lane sorts the same
+    // words; equal keys in any order give the same key)
     const int q = (R - L) >> 3;
-    double sm[8];
+    uint64_t sm[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) sm[i] = K[A[L + q * (i + 1)]];
+    for (int i = 0; i < 8; ++i) sm[i] = W[L + q * (i + 1)];
 #pragma unroll
-    for (int i = 1; i < 8; ++i)                              // (same data in every lane)
+    for (int i = 1; i < 8; ++i)
 #pragma unroll
       for (int j = i; j > 0; --j) {
-        const double lo = sm[j - 1], hi = sm[j];
+        const uint64_t lo = sm[j - 1], hi = sm[j];
         sm[j - 1] = lo < hi ? lo : hi;
         sm[j] = lo < hi ? hi : lo;
       }
-    const double pivot = sm[4];
+    const uint64_t pf = sm[4] & ~kOrdIdx;                    // key < pivot <=> w < pf
+    const uint64_t pc = pf | kOrdIdx;                        // key > pivot <=> w > pc
     bool lt = false, gt = false;
     int left = L, right = R + 1;
     const int rem = (R + 1 - L) & 31;
@@ -917,9 +930,8 @@ __global__ void __launch_bounds__(64) osd_order_kernel(OrderArgs a) {
       // examined next. Lane i < 32 holds left-stream key i (position L + i),
       // lane 32 + i right-stream key i (position R - i).
       const int pos = lane < 32 ? L + lane : R - (lane - 32);
-      const int iv = A[pos];
-      const double kv = K[iv];
-      const uint64_t ltm = __ballot(kv < pivot);
+      const uint64_t wv = W[pos];
+      const uint64_t ltm = __ballot(wv < pf);
       int cur = 0, dest = -1;
       bool ex = false;
       for (int s = 0; s < rem; ++s) {
@@ -935,30 +947,29 @@ __global__ void __launch_bounds__(64) osd_order_kernel(OrderArgs a) {
         }
       }
       if (lane == cur) dest = left;                          // moved to `left`, not examined
-      lt |= ex && kv < pivot;
-      gt |= ex && kv > pivot;
-      if (dest >= 0) A[dest] = (uint16_t)iv;
+      lt |= ex && wv < pf;
+      gt |= ex && wv > pc;
+      if (dest >= 0) W[dest] = wv;
       ord_fence();
     }
     // the 32-aligned middle [left, right): rows of 64 keys (8 vectors)
     const int M = right - left, nb = M >> 5;
-    int iv[EPL];
+    uint64_t ev[EPL];
     uint32_t byt[(EPL + 3) / 4];                             // row r's vector byte at bits 8 (r % 4)
     uint32_t mym = 0;
 #pragma unroll
     for (int r = 0; r < EPL; ++r) {
       if (64 * r >= M) break;
       const int o = 64 * r + lane;
-      iv[r] = A[left + (o < M ? o : 0)];
+      ev[r] = W[left + (o < M ? o : 0)];
     }
 #pragma unroll
     for (int r = 0; r < EPL; ++r) {
       if (64 * r >= M) break;
       const bool valid = 64 * r + lane < M;
-      const double kv = K[iv[r]];
-      lt |= valid && kv < pivot;
-      gt |= valid && kv > pivot;
-      const uint64_t bm = __ballot(valid && kv >= pivot);
+      lt |= valid && ev[r] < pf;
+      gt |= valid && ev[r] > pc;
+      const uint64_t bm = __ballot(valid && ev[r] >= pf);
       if ((lane >> 1) == r) mym = (lane & 1) ? (uint32_t)(bm >> 32) : (uint32_t)bm;
       const uint32_t by = (uint32_t)(bm >> (lane & 56)) & 0xffu;
       byt[r / 4] = (r % 4 ? byt[r / 4] : 0u) | (by << (8 * (r % 4)));
@@ -1013,7 +1024,7 @@ __global__ void __launch_bounds__(64) osd_order_kernel(OrderArgs a) {
         const uint32_t below = byte & ((1u << kk) - 1u);
         const int dst = (byte >> kk) & 1u ? vr - __builtin_popcount(byte) + __builtin_popcount(below)
                                           : vl + kk - __builtin_popcount(below);
-        A[dst] = (uint16_t)iv[r];
+        W[dst] = ev[r];
       }
     }
     ord_fence();
@@ -1035,11 +1046,11 @@ __global__ void __launch_bounds__(64) osd_order_kernel(OrderArgs a) {
     sp += (lany ? 1 : 0) + (gany ? 1 : 0);
     ord_fence();
   }
-  for (int i = lane; i < n; i += 64) perm[i] = A[i];
+  for (int i = lane; i < n; i += 64) perm[i] = (int32_t)(W[i] & kOrdIdx);
   if (lane == 0) a.tiepos[shot] = fallback ? -1 : n;
 }
 
-size_t osd_order_lds(int n) { return (size_t)10 * n + 96 * 4 + 512 * 2 + 16; }
+size_t osd_order_lds(int n) { return (size_t)8 * n + 96 * 4 + 512 * 2 + 16; }
 
 hipError_t launch_osd_order(const OrderArgs& a, long long count, hipStream_t stream) {
   const void* k = a.n <= 256 ? (const void*)&osd_order_kernel<4>

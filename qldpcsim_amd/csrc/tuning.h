@@ -12,7 +12,8 @@
     (defined(QLDPC_ABLATE) || defined(QLDPC_ABLATE_L) || defined(QLDPC_ABLATE_OSD) ||               \
      defined(QLDPC_OSD_TIMING) || defined(QLDPC_VN_PAIR) || defined(QLDPC_FLOOD_WPE) ||             \
      defined(QLDPC_VN_H) || defined(QLDPC_HBM_WAVES) || defined(QLDPC_HBM_UC) ||                    \
-     defined(QLDPC_OSD_WPE) || defined(QLDPC_OSD_PRIO) || defined(QLDPC_VN_PREINFO))
+     defined(QLDPC_OSD_WPE) || defined(QLDPC_OSD_PRIO) || defined(QLDPC_VN_PREINFO) ||                \
+     defined(QLDPC_ABLATE_ORD))
 #error "kernel tuning knobs are for experiment builds: add -DQLDPC_EXPERIMENTS"
 #endif
 
@@ -25,6 +26,9 @@
 #endif
 #ifndef QLDPC_ABLATE_OSD
 #define QLDPC_ABLATE_OSD 0   // osd_block_kernel: bit 0 skips phase D, bit 1 the engine
+#endif
+#ifndef QLDPC_ABLATE_ORD
+#define QLDPC_ABLATE_ORD 0   // osd_order_kernel: bit 0 skips the <= 256-key networks, bit 1 the partitions
 #endif
 #ifndef QLDPC_OSD_TIMING
 #define QLDPC_OSD_TIMING 0   // osd_block_kernel sums per-phase cycles into OsdArgs::prof (option osd_prof)
