@@ -256,8 +256,9 @@ __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
 //   D  every row applies its C to words w..: each update added a current
 //      pivot row = its block-start value + earlier pivot rows of the block.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t opaque_u32(uint32_t x) {
-  asm volatile("" : "+v"(x));
+// x with lane `l` replaced by the wave-uniform v (v_writelane_b32)
+__device__ __forceinline__ uint32_t write_lane(uint32_t x, uint32_t v, int l) {
+  asm("v_writelane_b32 %0, %1, m0" : "+v"(x) : "s"(v), "{m0}"(l));   // (gfx9: one SGPR operand, lane in M0)
   return x;
 }
 
@@ -273,8 +274,12 @@ __device__ __forceinline__ uint32_t wave_or32(uint32_t x) {
 // Phase B over the columns `cols` of one half-word (HI: bits 32..63, read
 // from hi[]) on the first SF compact slots, straight-line per column: one
 // ballot per slot masked by the slot's still-free rows (fm[s], a wave-uniform
-// lane mask in SGPRs), the first hit by scalar selects, the pivot's values by
-// a uniform switch on its slot + readlane, the elimination under exec masks.
+// lane mask in SGPRs); the slot that hits reads the pivot's values (readlane
+// under its compile-time slot index: no dispatch on the slot afterwards) and
+// clears the pivot's own column bit in the pivot row, so the elimination
+// needs no per-slot exclusion of the pivot row: within the block the row's
+// bits at this or earlier columns are never read again, and the engine's
+// lo/hi words are dropped at the block end (only cl/ch leave it).
 // Pivot k's compact position and column bit go to pk[k]; returns the pivot
 // count K.
 template <int SL, int SF, bool HI>
@@ -282,7 +287,6 @@ __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL]
                                           uint32_t (&ch)[SL], uint64_t (&fm)[SL], uint32_t cols, int K,
                                           int w, int lane, int& rank, int& nJ, bool& done, uint64_t& pivm,
                                           int rankH, int m, int& pkv) {
-  static_assert(SL <= 8, "the pivot-slot switch covers 8 slots");
   while (cols && !done) {
     // loop-carried scalars re-asserted wave-uniform: otherwise the compiler
     // keeps them per lane and turns the loop into an exec-masked one
@@ -292,13 +296,13 @@ __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL]
     nJ = __builtin_amdgcn_readfirstlane(nJ);
     pivm = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pivm >> 32)) << 32) |
            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pivm);
-    // next column with a pivot: the search loop only reads the state, so
-    // skipping dependent columns costs no register copies at the joins
-    // Slots are scanned in ascending order and the scan stops at the first
-    // hit (uniform branches): once rows fill up, slot 0 almost always holds
-    // the pivot; a select chain over all SF slots cost 7 instructions each.
-    int f = 0x7fffffff, bit = 0;
-    while (cols) {
+    // next column with a pivot: slots scanned in ascending order, the scan
+    // stops at the first hit (uniform branches) — once rows fill up, slot 0
+    // almost always holds the pivot. Dependent columns (no free row holds
+    // them) are skipped without touching the state; they are not in J.
+    int f = -1, bit = 0;
+    uint32_t plo = 0, phi = 0, pcl = 0, pch = 0;
+    while (cols && f < 0) {
       bit = (int)__builtin_ctz(cols);
       cols &= cols - 1;
       const uint32_t bm = 1u << bit;
@@ -306,46 +310,36 @@ __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL]
       for (int s = 0; s < SF; ++s) {
         const uint64_t c = __ballot(((HI ? hi[s] : lo[s]) & bm) != 0) & fm[s];
         if (c) {
-          f = 64 * s + (int)__builtin_ctzll(c);
+          const int fl = (int)__builtin_ctzll(c);
+          f = 64 * s + fl;
+          plo = __builtin_amdgcn_readlane((int)lo[s], fl);
+          phi = __builtin_amdgcn_readlane((int)hi[s], fl);
+          pcl = __builtin_amdgcn_readlane((int)cl[s], fl);
+          pch = __builtin_amdgcn_readlane((int)ch[s], fl);
+          fm[s] &= ~(1ull << fl);                     // no longer free
+          if (HI) hi[s] = write_lane(hi[s], phi & ~bm, fl);
+          else lo[s] = write_lane(lo[s], plo & ~bm, fl);
           break;
         }
       }
       f = __builtin_amdgcn_readfirstlane(f);
-      if (f != 0x7fffffff) break;                   // (dependent columns: not in J)
     }
-    if (f == 0x7fffffff) break;
-    const int fs = f >> 6, fl = f & 63;
-    uint32_t plo = 0, phi = 0, pcl = 0, pch = 0;
-    switch (fs) {                                   // uniform: one case runs, no select chains
-#define QLDPC_PIVOT_SLOT(S)                                              \
-  case S:                                                                \
-    if constexpr (S < SF) {                                              \
-      plo = __builtin_amdgcn_readlane((int)lo[S], fl);                   \
-      phi = __builtin_amdgcn_readlane((int)hi[S], fl);                   \
-      pcl = __builtin_amdgcn_readlane((int)cl[S], fl);                   \
-      pch = __builtin_amdgcn_readlane((int)ch[S], fl);                   \
-      fm[S] &= ~(1ull << fl);                       /* no longer free */ \
-    }                                                                    \
-    break;
-      QLDPC_PIVOT_SLOT(0) QLDPC_PIVOT_SLOT(1) QLDPC_PIVOT_SLOT(2) QLDPC_PIVOT_SLOT(3)
-      QLDPC_PIVOT_SLOT(4) QLDPC_PIVOT_SLOT(5) QLDPC_PIVOT_SLOT(6) QLDPC_PIVOT_SLOT(7)
-#undef QLDPC_PIVOT_SLOT
-      default: break;
-    }
+    if (f < 0) break;                               // (dependent columns: not in J)
     // (+ the pivot itself; the 64-bit form, (pch:pcl) ^ (1ull << K), was
     // miscompiled in the 128-VGPR spilling instance: wrong eliminations,
     // correct at 3 waves per SIMD without spills — tools/osd_check.py)
-    if (K < 32) pcl ^= 1u << K;
-    else pch ^= 1u << (K - 32);
+    {
+      const uint32_t kb = 1u << (K & 31);
+      pcl ^= K < 32 ? kb : 0u;
+      pch ^= K < 32 ? 0u : kb;
+    }
     // Rows holding a 1 (above and below) take the pivot: x ^= p & mask with
-    // mask = 0 / ~0 from the column bit (one bit-field extract), the pivot
-    // row itself excluded — branch-free (v_bitop3), no exec-mask round trip
-    // from a VALU compare through SALU per slot. The low half is done in HI.
-    const uint32_t me = opaque_u32(lane == fl ? 0u : ~0u);
+    // mask = 0 / ~0 from the column bit (one bit-field extract) — branch-free
+    // (v_bitop3), no exec-mask round trip from a VALU compare through SALU
+    // per slot. The low half is done in HI.
 #pragma unroll
     for (int s = 0; s < SF; ++s) {
-      uint32_t mk = (uint32_t)__builtin_amdgcn_sbfe((int)(HI ? hi[s] : lo[s]), bit, 1);   // 0 / -1
-      mk &= (s == fs) ? me : ~0u;
+      const uint32_t mk = (uint32_t)__builtin_amdgcn_sbfe((int)(HI ? hi[s] : lo[s]), bit, 1);   // 0 / -1
       if (!HI) lo[s] ^= plo & mk;
       hi[s] ^= phi & mk;
       cl[s] ^= pcl & mk;
@@ -363,21 +357,23 @@ __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL]
     ++rank;
     if (rank >= rankH || rank >= m) done = true;
     if (i == 0 && done) rank = -1;                  // column 0 alone reaches rank(H): the
-    done = __builtin_amdgcn_readfirstlane((int)done) != 0;   // greedy loop never breaks (:333-342)
+                                                    // greedy loop never breaks (:333-342)
   }
   return K;
 }
 
-// block_half on the smallest power-of-two slot count >= SF (code per count)
+// block_half on the smallest power-of-two slot count >= SF (code per count),
+// or (QLDPC_OSD_SFEXACT) on exactly SF slots
 template <int SL, int SFMAX, bool HI>
 __device__ __forceinline__ int block_half_n(int SF, uint32_t (&lo)[SL], uint32_t (&hi)[SL], uint32_t (&cl)[SL],
                                             uint32_t (&ch)[SL], uint64_t (&fm)[SL], uint32_t cols, int K,
                                             int w, int lane, int& rank, int& nJ, bool& done, uint64_t& pivm,
                                             int rankH, int m, int& pkv) {
   if constexpr (SFMAX > 1) {
-    if (SF <= SFMAX / 2)
-      return block_half_n<SL, SFMAX / 2, HI>(SF, lo, hi, cl, ch, fm, cols, K, w, lane, rank, nJ, done, pivm,
-                                             rankH, m, pkv);
+    if (QLDPC_OSD_SFEXACT ? SF <= SFMAX - 1 : SF <= SFMAX / 2)
+      return block_half_n<SL, QLDPC_OSD_SFEXACT ? SFMAX - 1 : SFMAX / 2, HI>(SF, lo, hi, cl, ch, fm, cols, K, w,
+                                                                            lane, rank, nJ, done, pivm, rankH,
+                                                                            m, pkv);
   }
   return block_half<SL, SFMAX, HI>(lo, hi, cl, ch, fm, cols, K, w, lane, rank, nJ, done, pivm, rankH, m, pkv);
 }
@@ -406,15 +402,26 @@ __device__ __forceinline__ uint64_t osd_gather_xor4(const uint64_t* tab, uint64_
 
 template <int NW, int W0>
 __device__ __forceinline__ void osd_apply_from(uint64_t (&R)[NW], uint64_t cm, const uint64_t* PW) {
+  // a pivot row's words W0.. in one read batch, or in two when more than
+  // QLDPC_OSD_DSPLIT words remain: the peak register need of phase D is the
+  // rows' state plus one batch
+  constexpr int NB = NW - W0, B1 = (QLDPC_OSD_DSPLIT > 0 && NB > QLDPC_OSD_DSPLIT) ? (NB + 1) / 2 : NB;
   while (cm) {
     const int k = (int)__builtin_ctzll(cm);
     cm &= cm - 1;
     const uint64_t* src = PW + k * NW;
-    uint64_t v[NW - W0];
+    uint64_t v[B1];
 #pragma unroll
-    for (int x = W0; x < NW; ++x) v[x - W0] = src[x];
+    for (int x = 0; x < B1; ++x) v[x] = src[W0 + x];
 #pragma unroll
-    for (int x = W0; x < NW; ++x) R[x] ^= v[x - W0];
+    for (int x = 0; x < B1; ++x) R[W0 + x] ^= v[x];
+    if constexpr (B1 < NB) {
+      uint64_t u[NB - B1];
+#pragma unroll
+      for (int x = 0; x < NB - B1; ++x) u[x] = src[W0 + B1 + x];
+#pragma unroll
+      for (int x = 0; x < NB - B1; ++x) R[W0 + B1 + x] ^= u[x];
+    }
   }
 }
 

@@ -13,7 +13,8 @@
      defined(QLDPC_OSD_TIMING) || defined(QLDPC_VN_PAIR) || defined(QLDPC_FLOOD_WPE) ||             \
      defined(QLDPC_VN_H) || defined(QLDPC_HBM_WAVES) || defined(QLDPC_HBM_UC) ||                    \
      defined(QLDPC_OSD_WPE) || defined(QLDPC_OSD_PRIO) || defined(QLDPC_VN_PREINFO) ||                \
-     defined(QLDPC_ABLATE_ORD))
+     defined(QLDPC_ABLATE_ORD) || defined(QLDPC_OSD_DSPLIT) ||                                     \
+     defined(QLDPC_OSD_SFEXACT))
 #error "kernel tuning knobs are for experiment builds: add -DQLDPC_EXPERIMENTS"
 #endif
 
@@ -56,6 +57,15 @@
 #ifndef QLDPC_OSD_PRIO
 #define QLDPC_OSD_PRIO 3     // osd_block_kernel: s_setprio of the engine wave during phase B (0: none;
                              // 1 and 3 both -3.3 % per launch, profiles/r04am/)
+#endif
+#ifndef QLDPC_OSD_DSPLIT
+#define QLDPC_OSD_DSPLIT 12  // osd_block_kernel phase D: pivot-row words read in two batches when more
+                             // than this many remain (0: one batch); 12: 93 -> 16 spilled VGPRs,
+                             // 26.85 -> 26.56 ms per 68,301 shots (profiles/r05/osd_dsplit_ab.jsonl)
+#endif
+#ifndef QLDPC_OSD_SFEXACT
+#define QLDPC_OSD_SFEXACT 0  // osd_block_kernel phase B: code for every free-slot count 1..SL (1), or for
+                             // powers of two only (0)
 #endif
 #ifndef QLDPC_VN_PREINFO
 #define QLDPC_VN_PREINFO 1     // ms_layered_kernel<DC, 1>: first VN adjacency words read at the layer head

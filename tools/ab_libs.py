@@ -33,7 +33,8 @@ def main():
                 path, _, opts = lib.partition("@")
                 env = dict(os.environ, QLDPC_LIB=os.path.abspath(path), QLDPC_OPTIONS=opts)
                 out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
-                                      "--cpu-seconds", "0", *shlex.split(cfg)],
+                                      "--cpu-seconds", "0", "--sim-legs", "", "--hbm-leg", "0",
+                                      *shlex.split(cfg)],
                                      env=env, capture_output=True, text=True, timeout=300)
                 line = [l for l in out.stdout.splitlines() if l.startswith("{")]
                 if not line:
