@@ -28,6 +28,7 @@
 #include "osd_kernels.h"
 #include "channel_kernels.h"
 #include "hbm_kernels.h"
+#include "tuning.h"
 
 using qldpc::DecodeArgs;
 
@@ -320,6 +321,7 @@ struct LaunchCfg {
   bool gtab = false;     // ms_flood_kernel: global tables, LDS = wave state only
   bool tlg = false;      // bp_team_lg_kernel: every table global, LDS image = layer pointers
   bool hbm = false;      // the LDS kernels cannot hold this schedule: hbm_tile_kernel (cached)
+  int msl_gt = 0;        // ms_layered_kernel<DC, 1> built with QLDPC_MSL_GT: tables left in global memory
   uint32_t gen = 0;      // g_opt.gen the configuration was built under
   int team = 0;          // bp_team_kernel: waves per half-shot (one workgroup), 0 = wave kernels
   const char* name = "";  // kernel name as rocprofv3 reports it
@@ -703,6 +705,11 @@ static void team_layout(const qldpc_code* c, int w, int* bytes, int* off_c2v, in
   *bytes = off;
 }
 
+// ms_layered_kernel's LDS image with QLDPC_MSL_GT: the layer-ordered blob
+// without its leading row table and its trailing filter words (both read
+// from global memory)
+static int msl_lds_bytes(const qldpc_schedule* s, int) { return s->l_off_vn_chk - s->l_off_lrow; }
+
 // The launch configuration of (schedule, algo), copied into *out under the
 // schedule's lock: a launch keeps its own consistent snapshot even if an
 // option change (qldpc_set_option) rebuilds the cached one meanwhile.
@@ -737,6 +744,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg* out) {
     // in round 2: at a fixed LDS budget it halves the waves per CU; removed)
     cfg.kernel = qldpc::select_ms_layered_kernel(dc, g, &cfg.name);
     use_lblob = cfg.kernel != nullptr;
+    cfg.msl_gt = use_lblob && g == 1 && s->l_off_ltab == 0 ? QLDPC_MSL_GT : 0;
   }
   cfg.lblob = use_lblob;
   cfg.gtab = gtab;
@@ -775,6 +783,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg* out) {
   HIP_TRY(qldpc::configure_kernel(cfg.kernel, max_lds));
   const int blob = gtab ? QLDPC_FLOOD_HDR
                         : cfg.tlg ? s->lg_lds_bytes
+                        : cfg.msl_gt ? msl_lds_bytes(s, cfg.msl_gt)
                         : (int)(use_lblob ? s->lblob.size() : s->blob.size());
   // BP kernels stage NumPy's libm tables behind every slice (DecodeArgs::off_libm)
   const int libm = algo == QLDPC_ALGO_BP ? (int)sizeof(qldpc_libm_tab) : 0;
@@ -1066,6 +1075,10 @@ extern "C" int qldpc_decode_device_ex(const qldpc_code* code, const qldpc_schedu
     a.off_row_ptr = sched->l_off_adj_info;
     a.off_chunk_dmax = sched->l_off_adj_dmax;
     a.off_vn_chk = sched->l_off_vn_chk;
+    if (cfg->msl_gt) {  // row table (offset 0) and filter words (last) stay global
+      a.lds_skip = sched->l_off_lrow;
+      a.blob_bytes = msl_lds_bytes(sched, cfg->msl_gt);
+    }
   }
   if (cfg->team) team_layout(code, cfg->team, &a.wave_bytes, &a.off_c2v, &a.off_synw, &a.off_parw, &a.off_red);
   if (cfg->tlg) {  // bp_team_lg_kernel: layer pointers in LDS, every table global

@@ -49,6 +49,7 @@ struct DecodeArgs {
   int syn_bits, eh_bits;
   int wm, wn;                 // ceil(m / 64), ceil(n / 64)
   int off_libm;               // BP: LDS byte offset of the qldpc_libm_tab image (after every slice)
+  int lds_skip;               // ms_layered_kernel (QLDPC_MSL_GT): blob bytes before the LDS image
 };
 
 // `name` (nullable) receives the kernel's name as rocprofv3 reports it

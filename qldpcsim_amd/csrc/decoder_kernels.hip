@@ -1497,20 +1497,36 @@ __device__ __forceinline__ void cn_layer(const DecodeArgs& a, const uint32_t* lt
 template <int DC, int G>
 __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  // QLDPC_MSL_GT (the one-lane-per-check instance): the row table [Q][8] and
+  // the filter words stay in global memory (L1/L2-resident; the LDS image
+  // starts a.lds_skip bytes in, after the row table, and ends before the
+  // filter words), so a CU holds 8 waves' state instead of 7 (LP118_2: 39.9
+  // -> 36.5 ms per p = 0.1 launch; loading the next layer's row words a layer
+  // ahead measured slower, profiles/r05/msl_global_tables_ab.json)
+  constexpr int GT = G == 1 ? QLDPC_MSL_GT : 0;
+  const int sk = GT ? a.lds_skip : 0;
   {
-    const uint4* src = (const uint4*)a.blob;
+    const uint4* src = (const uint4*)(a.blob + sk);
     uint4* dst = (uint4*)lds;
     const int nvec = a.blob_bytes >> 4;
     for (int i = threadIdx.x; i < nvec; i += blockDim.x) dst[i] = src[i];
   }
   __syncthreads();
-  const uint32_t* ltab = (const uint32_t*)(lds + a.off_cn_tab);      // [Q][8]
-  const uint16_t* lrow = (const uint16_t*)(lds + a.off_lay_rows);    // [Q]
-  const uint16_t* lay_ptr = (const uint16_t*)(lds + a.off_lay_ptr);  // [L+1]
-  const uint16_t* adj_ptr = (const uint16_t*)(lds + a.off_adj_ptr);  // [L+1]
-  const uint32_t* adj_info = (const uint32_t*)(lds + a.off_row_ptr); // [A] var<<21 | deg<<16 | csc start
-  const uint8_t* adj_dmax = (const uint8_t*)(lds + a.off_chunk_dmax);// [L] max degree per layer
-  const uint32_t* avar = (const uint32_t*)(lds + a.off_vn_chk);      // [n] filter word per variable
+  const uint32_t* ltab_l = (const uint32_t*)(lds + a.off_cn_tab);    // [Q][8]
+  const uint32_t* ltab_g = (const uint32_t*)(a.blob + a.off_cn_tab); // [Q][8] global (GT)
+  const uint32_t* ltab = [&]() {
+    if constexpr (GT != 0) return ltab_g;
+    else return ltab_l;
+  }();
+  const uint16_t* lrow = (const uint16_t*)(lds + a.off_lay_rows - sk);    // [Q]
+  const uint16_t* lay_ptr = (const uint16_t*)(lds + a.off_lay_ptr - sk);  // [L+1]
+  const uint16_t* adj_ptr = (const uint16_t*)(lds + a.off_adj_ptr - sk);  // [L+1]
+  const uint32_t* adj_info = (const uint32_t*)(lds + a.off_row_ptr - sk); // [A] var<<21 | deg<<16 | csc start
+  const uint8_t* adj_dmax = (const uint8_t*)(lds + a.off_chunk_dmax - sk);// [L] max degree per layer
+  const uint32_t* avar = [&]() {                                         // [n] filter word per variable
+    if constexpr (GT != 0) return a.avar;
+    else return (const uint32_t*)(lds + a.off_vn_chk - sk);
+  }();
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int waves = blockDim.x >> 6;

@@ -14,7 +14,7 @@
      defined(QLDPC_VN_H) || defined(QLDPC_HBM_WAVES) || defined(QLDPC_HBM_UC) ||                    \
      defined(QLDPC_OSD_WPE) || defined(QLDPC_OSD_PRIO) || defined(QLDPC_VN_PREINFO) ||                \
      defined(QLDPC_ABLATE_ORD) || defined(QLDPC_OSD_DSPLIT) ||                                     \
-     defined(QLDPC_OSD_SFEXACT))
+     defined(QLDPC_OSD_SFEXACT) || defined(QLDPC_MSL_GT))
 #error "kernel tuning knobs are for experiment builds: add -DQLDPC_EXPERIMENTS"
 #endif
 
@@ -66,6 +66,10 @@
 #ifndef QLDPC_OSD_SFEXACT
 #define QLDPC_OSD_SFEXACT 0  // osd_block_kernel phase B: code for every free-slot count 1..SL (1), or for
                              // powers of two only (0)
+#endif
+#ifndef QLDPC_MSL_GT
+#define QLDPC_MSL_GT 1       // ms_layered_kernel<DC, 1>: row table and filter words in global memory, 8
+                             // waves per CU (1: LP118_2 p = 0.1 39.9 -> 36.5 ms per launch), or in LDS (0)
 #endif
 #ifndef QLDPC_VN_PREINFO
 #define QLDPC_VN_PREINFO 1     // ms_layered_kernel<DC, 1>: first VN adjacency words read at the layer head
