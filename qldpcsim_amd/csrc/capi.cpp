@@ -1622,8 +1622,8 @@ static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t*
   const int mr = rt * bblk;                          // its row slots
   const int base = align16(4 * n + 4 * (m + 2) + n) + (order == 1 ? 4 * setdiff_table_ints(n) : 0);
   const int lds_col = base + 8 * nw * (1 + 2 * 16 + 2) + 4 * 32 + 16;         // emask, candidate / xrow rows, slots, misc
-  const int lds_blk = base + 8 * nw * (1 + 64) + 8 * 64 + 8 * 2 * mr + 4 * 3 * mr + 4 * 64 + 64;
-                      // emask, PW, CT, Wd / Cm, pkof / pidx / crow, pk, misc
+  const int lds_blk = base + 8 * nw * (1 + 64 + (QLDPC_OSD_PAIRS ? 32 : 0)) + 8 * 64 + 8 * 2 * mr + 4 * 3 * mr + 4 * 64 + 64;
+                      // emask, PW, PX, CT, Wd / Cm, pkof / pidx / crow, pk, misc
   int dev = 0, max_lds = 0;
   HIP_TRY(hipGetDevice(&dev));
   HIP_TRY(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));

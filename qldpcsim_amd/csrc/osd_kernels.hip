@@ -315,7 +315,7 @@ __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL]
           plo = __builtin_amdgcn_readlane((int)lo[s], fl);
           phi = __builtin_amdgcn_readlane((int)hi[s], fl);
           pcl = __builtin_amdgcn_readlane((int)cl[s], fl);
-          pch = __builtin_amdgcn_readlane((int)ch[s], fl);
+          if (HI) pch = __builtin_amdgcn_readlane((int)ch[s], fl);
           fm[s] &= ~(1ull << fl);                     // no longer free
           if (HI) hi[s] = write_lane(hi[s], phi & ~bm, fl);
           else lo[s] = write_lane(lo[s], plo & ~bm, fl);
@@ -328,22 +328,26 @@ __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL]
     // (+ the pivot itself; the 64-bit form, (pch:pcl) ^ (1ull << K), was
     // miscompiled in the 128-VGPR spilling instance: wrong eliminations,
     // correct at 3 waves per SIMD without spills — tools/osd_check.py)
-    {
+    if (HI) {
       const uint32_t kb = 1u << (K & 31);
       pcl ^= K < 32 ? kb : 0u;
       pch ^= K < 32 ? 0u : kb;
+    } else {
+      pcl ^= 1u << K;                               // (low half: K < 32)
     }
     // Rows holding a 1 (above and below) take the pivot: x ^= p & mask with
     // mask = 0 / ~0 from the column bit (one bit-field extract) — branch-free
     // (v_bitop3), no exec-mask round trip from a VALU compare through SALU
-    // per slot. The low half is done in HI.
+    // per slot. The low half is done in HI. In the low half the block has
+    // fewer than 32 pivots, so every C word's high half is still zero (no
+    // ch update).
 #pragma unroll
     for (int s = 0; s < SF; ++s) {
       const uint32_t mk = (uint32_t)__builtin_amdgcn_sbfe((int)(HI ? hi[s] : lo[s]), bit, 1);   // 0 / -1
       if (!HI) lo[s] ^= plo & mk;
       hi[s] ^= phi & mk;
       cl[s] ^= pcl & mk;
-      ch[s] ^= pch & mk;
+      if (HI) ch[s] ^= pch & mk;
     }
     const int wb = (HI ? 32 : 0) + bit;
     const int i = 64 * w + wb;
@@ -401,15 +405,24 @@ __device__ __forceinline__ uint64_t osd_gather_xor4(const uint64_t* tab, uint64_
 }
 
 template <int NW, int W0>
-__device__ __forceinline__ void osd_apply_from(uint64_t (&R)[NW], uint64_t cm, const uint64_t* PW) {
+__device__ __forceinline__ void osd_apply_from(uint64_t (&R)[NW], uint64_t cm, const uint64_t* PW, const uint64_t* PX) {
   // a pivot row's words W0.. in one read batch, or in two when more than
   // QLDPC_OSD_DSPLIT words remain: the peak register need of phase D is the
-  // rows' state plus one batch
+  // rows' state plus one batch. QLDPC_OSD_PAIRS: pivots taken two at a time
+  // (k = 2j, 2j + 1), PX[j] = PW[2j] ^ PW[2j + 1]: one row read per nonzero
+  // pair of cm's bits instead of one per bit
   constexpr int NB = NW - W0, B1 = (QLDPC_OSD_DSPLIT > 0 && NB > QLDPC_OSD_DSPLIT) ? (NB + 1) / 2 : NB;
-  while (cm) {
-    const int k = (int)__builtin_ctzll(cm);
-    cm &= cm - 1;
-    const uint64_t* src = PW + k * NW;
+  uint64_t it = QLDPC_OSD_PAIRS ? (cm | (cm >> 1)) & 0x5555555555555555ull : cm;
+  while (it) {
+    const int k = (int)__builtin_ctzll(it);
+    it &= it - 1;
+    const uint64_t* src;
+    if constexpr (QLDPC_OSD_PAIRS != 0) {
+      const int b = (int)(cm >> k) & 3;
+      src = b == 3 ? PX + (k >> 1) * NW : PW + (k + (b >> 1)) * NW;
+    } else {
+      src = PW + k * NW;
+    }
     uint64_t v[B1];
 #pragma unroll
     for (int x = 0; x < B1; ++x) v[x] = src[W0 + x];
@@ -427,10 +440,11 @@ __device__ __forceinline__ void osd_apply_from(uint64_t (&R)[NW], uint64_t cm, c
 
 // R[x] ^= PW[k][x] for x >= w and every set bit k of cm (w wave-uniform)
 template <int NW, int W0 = 0>
-__device__ __forceinline__ void osd_apply_rows(uint64_t (&R)[NW], uint64_t cm, const uint64_t* PW, int w) {
+__device__ __forceinline__ void osd_apply_rows(uint64_t (&R)[NW], uint64_t cm, const uint64_t* PW, const uint64_t* PX,
+                                               int w) {
   if constexpr (W0 < NW) {
-    if (w == W0) osd_apply_from<NW, W0>(R, cm, PW);
-    else osd_apply_rows<NW, W0 + 1>(R, cm, PW, w);
+    if (w == W0) osd_apply_from<NW, W0>(R, cm, PW, PX);
+    else osd_apply_rows<NW, W0 + 1>(R, cm, PW, PX, w);
   }
 }
 
@@ -441,7 +455,7 @@ __device__ __forceinline__ void osd_apply_rows(uint64_t (&R)[NW], uint64_t cm, c
 template <int NW, int SL, int RT>
 __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_eu(RT == 2 ? QLDPC_OSD_WPE : 1))) osd_block_kernel(OsdArgs a) {
   // LDS: inv_perm[n] | J list [m+2] | inJ bytes [n] | emask [NW] | Wd [MR] | Cm [MR] |
-  //      PW [64][NW] | CT [64] | pkof [MR] | pidx [MR] | crow [MR] | pk [64] | misc [16] | set table
+  //      PW [64][NW] | PX [32][NW] (QLDPC_OSD_PAIRS) | CT [64] | pkof [MR] | pidx [MR] | crow [MR] | pk [64] | misc [16] | set table
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int m = a.m, n = a.n;
   const int B = blockDim.x, MR = RT * B;
@@ -452,7 +466,8 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
   uint64_t* Wd = emask + NW;
   uint64_t* Cm = Wd + MR;
   uint64_t* PW = Cm + MR;                            // [64][NW]
-  uint64_t* CT = PW + 64 * NW;                       // C of this block's pivot by its column bit
+  uint64_t* PX = PW + 64 * NW;                       // [32][NW] pivot pairs (QLDPC_OSD_PAIRS)
+  uint64_t* CT = PX + (QLDPC_OSD_PAIRS ? 32 * NW : 0);   // C of this block's pivot by its column bit
   int* pkof = (int*)(CT + 64);                       // pivot tag per row: 64 w + k, -1 none
   int* pidx = pkof + MR;                             // pivot index of each row (m: none)
   int* crow = pidx + MR;                             // compact position -> row (free rows)
@@ -658,6 +673,17 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
       }
     }
     __syncthreads();
+    if constexpr (QLDPC_OSD_PAIRS != 0) {
+      // pair rows PX[j] = PW[2j] ^ PW[2j + 1], words w.. (pairs of this block's pivots)
+      if (K > 1) {                                    // (uniform)
+        const int np = K >> 1, nx = NW - w;
+        for (int i = t; i < np * nx; i += B) {
+          const int j = i / nx, x = w + i - j * nx;
+          PX[j * NW + x] = PW[2 * j * NW + x] ^ PW[(2 * j + 1) * NW + x];
+        }
+        __syncthreads();
+      }
+    }
     QLDPC_TICK(4);
     // D: every row applies its combination of this block's pivot rows
 #pragma unroll
@@ -681,7 +707,7 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
       // compile-time one per block (switch on w), so a pivot row's words are
       // all read before any XOR — one LDS round trip per pivot row instead
       // of one per word behind a uniform branch.
-      osd_apply_rows<NW>(R[h], cm, PW, w);
+      osd_apply_rows<NW>(R[h], cm, PW, PX, w);
     }
     QLDPC_TICK(5);
   }

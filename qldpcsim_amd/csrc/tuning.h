@@ -14,7 +14,8 @@
      defined(QLDPC_VN_H) || defined(QLDPC_HBM_WAVES) || defined(QLDPC_HBM_UC) ||                    \
      defined(QLDPC_OSD_WPE) || defined(QLDPC_OSD_PRIO) || defined(QLDPC_VN_PREINFO) ||                \
      defined(QLDPC_ABLATE_ORD) || defined(QLDPC_OSD_DSPLIT) ||                                     \
-     defined(QLDPC_OSD_SFEXACT) || defined(QLDPC_MSL_GT))
+     defined(QLDPC_OSD_SFEXACT) || defined(QLDPC_MSL_GT) ||                                      \
+     defined(QLDPC_OSD_PAIRS))
 #error "kernel tuning knobs are for experiment builds: add -DQLDPC_EXPERIMENTS"
 #endif
 
@@ -66,6 +67,11 @@
 #ifndef QLDPC_OSD_SFEXACT
 #define QLDPC_OSD_SFEXACT 0  // osd_block_kernel phase B: code for every free-slot count 1..SL (1), or for
                              // powers of two only (0)
+#endif
+#ifndef QLDPC_OSD_PAIRS
+#define QLDPC_OSD_PAIRS 1    // osd_block_kernel phase D: this block's pivots applied two at a time from
+                             // a table of pair XORs (one LDS row read per nonzero bit pair): 22.82 ->
+                             // 22.38 ms per 68,301 shots (profiles/r05/osd_pairs_ab.jsonl)
 #endif
 #ifndef QLDPC_MSL_GT
 #define QLDPC_MSL_GT 1       // ms_layered_kernel<DC, 1>: row table and filter words in global memory, 8
