@@ -78,6 +78,7 @@
                              // waves per CU (1: LP118_2 p = 0.1 39.9 -> 36.5 ms per launch), or in LDS (0)
 #endif
 #ifndef QLDPC_VN_PREINFO
-#define QLDPC_VN_PREINFO 1     // ms_layered_kernel<DC, 1>: first VN adjacency words read at the layer head
-                               // (-0.85 % per LP118_2 p = 0.1 launch, profiles/r04as/)
+#define QLDPC_VN_PREINFO 0     // ms_layered_kernel<DC, 1>: first VN adjacency words read at the layer head
+                               // (-0.85 % per LP118_2 p = 0.1 launch at 7 waves per CU, profiles/r04as/;
+                               // +1.5 % at 8 waves, profiles/r05/msl_vn_knobs_ab.json)
 #endif
