@@ -282,6 +282,38 @@ def test_ms_layered_kernels_match_oracle(dec, kernel, code, qopt):
     np.testing.assert_array_equal((r.flags & 2) != 0, (fl & 1) != 0)
 
 
+@pytest.mark.parametrize("nlayers", [2, 3, 5])
+def test_ms_layered_g1_multi_trip_layers(dec, nlayers, qopt):
+    """The one-lane-per-check instance on layers of more than 64 rows (several
+    check-node trips per layer, row words from the global table, round 5):
+    LP118_2's rows cut into 2-5 contiguous layers of 90-225 rows (one layer of
+    every row is flooding and takes the flooding kernel), bit-exact vs the
+    oracle."""
+    from oracle import oracle
+    from qldpcsim_amd import _lib, codes, schedule
+    Hx, Hz = codes.load_code("LP118_2")
+    m = Hz.shape[0]
+    cuts = np.linspace(0, m, nlayers + 1).astype(int)
+    layers = [np.arange(cuts[i], cuts[i + 1]) for i in range(nlayers)]
+    lp, lr = schedule.pack_layers(layers, m)
+    qopt(ms_lanes_per_check=1)
+    rng = np.random.default_rng(17)
+    syn = np.concatenate([rng.integers(0, 2, (64, m), dtype=np.uint8),
+                          _channel(Hx, Hz, 0.05, 192, 9)[0]])
+    code_h = _lib.code_for(Hz)
+    code_h._sched.clear()
+    try:
+        r = dec.decode_batch(Hz, syn, 0.05 / 3, 25, algo="MS", want_post=True, layer_ptr=lp, layer_rows=lr)
+        nm = _lib.kernel_name(Hz, lp, lr, "MS")
+        assert nm == "ms_layered_kernel<8, 1>", nm
+    finally:
+        code_h._sched.clear()
+    e, it, post, fl = oracle.decode_batch("MS", Hz, syn, 0.05 / 3, 25, lp, lr)
+    np.testing.assert_array_equal(r.iters, it)
+    np.testing.assert_array_equal(r.ehat, e)
+    np.testing.assert_array_equal(r.post.view(np.uint64), post.view(np.uint64))
+
+
 def test_ms_layered_large_mixed_batch(dec):
     """The default layered kernel over a batch large enough that the work
     queue hands out multi-half-shot chunks, with decodes of very different
