@@ -34,6 +34,7 @@
 
 #include "decoder_kernels.h"
 #include "tuning.h"
+#include "kargs.h"
 #include "../../include/qldpc_libm.h"
 
 namespace qldpc {
@@ -60,6 +61,8 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 __device__ __forceinline__ uint64_t ballot(int pred) { return __ballot(pred); }
+
+__device__ __forceinline__ const DecodeArgs& kargs_fresh() { return kargs_fresh<DecodeArgs>(); }
 
 // LDS (address space 3) access through a 32-bit byte address held in a VGPR
 // (ds_read / ds_write directly; a generic pointer would become flat_load).
@@ -1548,16 +1551,23 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
     int iters = a.max_iter;
     bool conv = false;
     const double L = a.L;
-    load_syndrome_bits<8>(a, hs, synw, lane);
-    for (int j = lane; j < n; j += 64) colS[j] = 0.0f;          // post = L, c2v = 0 (:148-150)
-    for (int p = lane; p < a.E; p += 64) c2v[p] = 0.0f;
+    {
+      const DecodeArgs& ak = QLDPC_MSL_KARGS ? kargs_fresh() : a;
+      load_syndrome_bits<8>(ak, hs, synw, lane);
+      for (int j = lane; j < n; j += 64) colS[j] = 0.0f;          // post = L, c2v = 0 (:148-150)
+      for (int p = lane; p < ak.E; p += 64) c2v[p] = 0.0f;
+    }
     wave_sync();
     // filter parities of the syndrome (B) and of the hard decisions (F: all
     // variables start at post = L, so all ones iff L < 0)
     uint32_t bl = 0;
-    for (int c = lane; c < m; c += 64) bl ^= ((synw[c >> 5] >> (c & 31)) & 1u) ? a.wc[c] : 0u;
+    uint32_t F;
+    {
+      const DecodeArgs& ak = QLDPC_MSL_KARGS ? kargs_fresh() : a;
+      for (int c = lane; c < m; c += 64) bl ^= ((synw[c >> 5] >> (c & 31)) & 1u) ? ak.wc[c] : 0u;
+      F = (L < 0.0) ? ak.filt_all : 0u;
+    }
     const uint32_t B = wave_xor(bl);
-    uint32_t F = (L < 0.0) ? a.filt_all : 0u;
     bool first = true;
     for (int it = 0; it < a.max_iter && !conv; ++it) {
       for (int l = 0; l < a.n_layers; ++l) {
@@ -1614,7 +1624,7 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
         if constexpr ((QLDPC_ABLATE_L & 4) == 0) F ^= wave_xor(acc);
         wave_sync();
         // stop test (:175-176): filters first, the exact test only if they pass
-        if (F == B && layered_full_check<DC>(a, colS, synw, lane, thr)) {
+        if (F == B && layered_full_check<DC>(QLDPC_MSL_KARGS ? kargs_fresh() : a, colS, synw, lane, thr)) {
           iters = it + 1;
           conv = true;
           break;
@@ -1622,11 +1632,14 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
       }
     }
     // ê, posteriors in original order (post = L + (f64)S, decoders.py:173-174)
-    write_outputs_batched<4>(a, hs, lane, [&](int v) { return L + (double)colS[v]; });
-    const uint64_t b1 = ballot((fl & FLAG_MIN_ZERO) != 0);
-    if (lane == 0) {
-      a.iters[hs] = iters;
-      if (a.flags) a.flags[hs] = (int32_t)((b1 ? FLAG_MIN_ZERO : 0) | (conv ? FLAG_CONVERGED : 0));
+    {
+      const DecodeArgs& ak = QLDPC_MSL_KARGS ? kargs_fresh() : a;
+      write_outputs_batched<4>(ak, hs, lane, [&](int v) { return L + (double)colS[v]; });
+      const uint64_t b1 = ballot((fl & FLAG_MIN_ZERO) != 0);
+      if (lane == 0) {
+        ak.iters[hs] = iters;
+        if (ak.flags) ak.flags[hs] = (int32_t)((b1 ? FLAG_MIN_ZERO : 0) | (conv ? FLAG_CONVERGED : 0));
+      }
     }
     wave_sync();
   }

@@ -15,7 +15,7 @@
      defined(QLDPC_OSD_WPE) || defined(QLDPC_OSD_PRIO) || defined(QLDPC_VN_PREINFO) ||                \
      defined(QLDPC_ABLATE_ORD) || defined(QLDPC_OSD_DSPLIT) ||                                     \
      defined(QLDPC_OSD_SFEXACT) || defined(QLDPC_MSL_GT) ||                                      \
-     defined(QLDPC_OSD_PAIRS))
+     defined(QLDPC_OSD_PAIRS) || defined(QLDPC_MSL_KARGS))
 #error "kernel tuning knobs are for experiment builds: add -DQLDPC_EXPERIMENTS"
 #endif
 
@@ -72,6 +72,11 @@
 #define QLDPC_OSD_PAIRS 1    // osd_block_kernel phase D: this block's pivots applied two at a time from
                              // a table of pair XORs (one LDS row read per nonzero bit pair): 22.82 ->
                              // 22.38 ms per 68,301 shots (profiles/r05/osd_pairs_ab.jsonl)
+#endif
+#ifndef QLDPC_MSL_KARGS
+#define QLDPC_MSL_KARGS 1    // ms_layered_kernel: arguments used only outside the layer loops reloaded
+                             // from the kernarg segment at their use (125 -> 16 spilled SGPRs; LP118_2
+                             // p = 0.1 35.78 -> 35.07 ms per launch, profiles/r05/msl_kargs_ab.json)
 #endif
 #ifndef QLDPC_MSL_GT
 #define QLDPC_MSL_GT 1       // ms_layered_kernel<DC, 1>: row table and filter words in global memory, 8
