@@ -1023,6 +1023,20 @@ extern "C" int qldpc_decode_device(const qldpc_code* code, const qldpc_schedule*
                                 QLDPC_FMT_BYTES, d_iters, d_post, d_flags, stream);
 }
 
+// The BP check node's saturated value (decoder_kernels.hip, cn_bp_word): at
+// |th2| = 1 the reference clips th2 to +-(1 - eps) (decoders.py:256-258), so
+// c2v = +-2 atanh(1 - eps) — computed here by the restated SVML atanh the
+// kernels and the oracle share (include/qldpc_libm.h), the same expression
+// as the full path; not finite (eps <= 0) turns the fast path off.
+static void bp_saturation(double eps, double* csat, uint32_t* sat_hi) {
+  double th2 = 1.0;
+  th2 = (std::fabs(th2) >= 1.0 - eps) ? std::copysign(std::fabs(th2) - eps, th2) : th2;
+  const double v = 2.0 * qldpc_atanh(th2);
+  const bool on = std::isfinite(v);
+  *csat = on ? v : 0.0;
+  *sat_hi = on ? 0x40338000u : 0x7ff00000u;            // |x| >= 19.5 (high word, sign cleared)
+}
+
 extern "C" int qldpc_decode_device_ex(const qldpc_code* code, const qldpc_schedule* sched_c, int algo,
                                       const void* d_syn, int syn_format, int64_t batch, double p, int max_iter,
                                       double beta, double eps, void* d_ehat, int ehat_format, int32_t* d_iters,
@@ -1118,6 +1132,7 @@ extern "C" int qldpc_decode_device_ex(const qldpc_code* code, const qldpc_schedu
   a.L32 = (float)a.L;
   a.beta = beta;
   a.eps = eps;
+  bp_saturation(eps, &a.bp_csat, &a.bp_sat_hi);
   a.max_iter = max_iter;
   a.wc = code->d_wc;
   a.rtab = code->d_rtab;

@@ -50,6 +50,10 @@ struct DecodeArgs {
   int wm, wn;                 // ceil(m / 64), ceil(n / 64)
   int off_libm;               // BP: LDS byte offset of the qldpc_libm_tab image (after every slice)
   int lds_skip;               // ms_layered_kernel (QLDPC_MSL_GT): blob bytes before the LDS image
+  // BP saturated check nodes (decoder_kernels.hip, cn_bp_word): c2v magnitude
+  // 2 atanh(1 - eps) and the |x| >= 19.5 high-word threshold (0x7ff00000: off)
+  double bp_csat;
+  uint32_t bp_sat_hi;
 };
 
 // `name` (nullable) receives the kernel's name as rocprofv3 reports it

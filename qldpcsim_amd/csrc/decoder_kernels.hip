@@ -61,6 +61,10 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 __device__ __forceinline__ uint64_t ballot(int pred) { return __ballot(pred); }
+// the same from a bool: the wave's compare mask itself (s_and with exec). The
+// int form above materialises the predicate (v_cndmask) and compares it again
+// (v_cmp_ne) — two VALU ops per ballot, kept where the code is profiled as is.
+__device__ __forceinline__ uint64_t ballot_b(bool pred) { return __builtin_amdgcn_ballot_w64(pred); }
 
 __device__ __forceinline__ const DecodeArgs& kargs_fresh() { return kargs_fresh<DecodeArgs>(); }
 
@@ -110,9 +114,9 @@ __device__ __forceinline__ double np_sum_lt8(const double* a, int n) {
 }
 
 __device__ __forceinline__ double np_sum_col(const double* a, int n) {
-  if (__builtin_expect(ballot(n >= 8) != 0, 0)) return np_pairwise_sum(a, n);
-  if (ballot(n > 3) == 0) return np_sum_lt8<3>(a, n);
-  if (ballot(n > 5) == 0) return np_sum_lt8<5>(a, n);
+  if (__builtin_expect(ballot_b(n >= 8) != 0, 0)) return np_pairwise_sum(a, n);
+  if (ballot_b(n > 3) == 0) return np_sum_lt8<3>(a, n);
+  if (ballot_b(n > 5) == 0) return np_sum_lt8<5>(a, n);
   return np_sum_lt8<7>(a, n);
 }
 
@@ -1664,8 +1668,21 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
 // Team-wide stop tests go through LDS slots (double-buffered, one barrier);
 // layered: parity filters posted per wave (see the layered branch).
 // ---------------------------------------------------------------------------
-// edge k of a check whose table word t (row table entry 8c + k) is given
-template <int DC>
+// Saturated check nodes. NumPy's tanh is +-1.0 exactly for |x| >= 19.5: the
+// interval [16, 24) evaluates 1 + y r(y) with |y r(y)| ~ 2 exp(-2|x|) <=
+// 2.3e-17, below half an ulp of 1 (2^-54), and [24, inf) has the constant
+// polynomial 1 (include/qldpc_numpy_tables.h; checked on the host restatement
+// and against NumPy, tests/test_libm.py). When every edge of a check has
+// |v2c / 2| >= 19.5, all its t_k are +-1, np.prod is +-1, th2 = P / t_k is
+// +-1 and clips to +-(1 - eps) (decoders.py:256-258), so c2v_k = +-2
+// atanh(1 - eps): one constant, DecodeArgs::bp_csat (capi.cpp, the same
+// restated atanh). A finite |x| is >= 19.5 iff its high word (sign cleared)
+// is >= 0x40338000 (19.5's low word is 0): DecodeArgs::bp_sat_hi, or
+// 0x7ff00000 (never) when the constant is not finite (eps <= 0: atanh(1)).
+
+// edge k of a check whose table word t (row table entry 8c + k) is given;
+// SAT: with the saturated-check fast path
+template <int DC, bool SAT>
 __device__ __forceinline__ uint32_t cn_bp_word(const DecodeArgs& a, const qldpc_libm_tab* lt, uint32_t t, bool valid,
                                                int k, int lane, uint32_t synb, const double* post, double* c2v,
                                                int& fl) {
@@ -1674,12 +1691,30 @@ __device__ __forceinline__ uint32_t cn_bp_word(const DecodeArgs& a, const qldpc_
   // loads and computes (t = 0 for a pad edge / check: variable 0, position
   // 0, in bounds) and the pad lanes' values are replaced by selects — no
   // exec-masked branches around the loads and the tanh
-  if (ballot(valid) == 0) return 0u;
+  if (ballot_b(valid) == 0) return 0u;
   const int j = (int)((t & 0xffffu) >> 3), p = (int)(t >> 18);
   const double pjr = post[j];
   const double x = (pjr - c2v[p]) / 2.0;                      // v2c (:269)
+  // saturated (finite, |x| >= 19.5): the high word (sign cleared) in
+  // [bp_sat_hi, 0x7ff00000), one unsigned compare after the subtraction
+  const uint32_t xh = (uint32_t)(__builtin_bit_cast(uint64_t, x) >> 32) & 0x7fffffffu;
+  const uint32_t shi = a.bp_sat_hi;
+  const bool unsat = xh - shi >= 0x7ff00000u - shi;
+  if (SAT && ballot_b(ek & unsat) == 0) {
+    // every edge of the wave's checks saturated: t_k = sign(x_k), P = the
+    // product of the group's signs (pad edges: +1), the message's sign =
+    // sign(P / t_k), then the syndrome's (:260-261)
+    const double csat = kargs_fresh<DecodeArgs>().bp_csat;
+    const uint64_t nb = ballot_b(ek && x < 0.0);
+    const uint32_t gs = (uint32_t)(nb >> (lane & 56)) & 0xffu;
+    const uint32_t neg = ((uint32_t)__builtin_popcount(gs) ^ (gs >> (lane & 7)) ^ synb) & 1u;
+    if (ek) c2v[p] = neg ? -csat : csat;
+    const uint64_t hb = ballot_b(ek && pjr < 0.0);
+    const uint32_t par = (uint32_t)__builtin_popcount((uint32_t)(hb >> (lane & 56)) & 0xffu) & 1u;
+    return valid ? (par ^ synb) : 0u;
+  }
   double th;                                                  // np.tanh (:254)
-  if (__builtin_expect(ballot(!(__builtin_fabs(x) < 0x1p1023)) != 0, 0))
+  if (__builtin_expect(ballot_b(!(__builtin_fabs(x) < 0x1p1023)) != 0, 0))
     th = qldpc_tanh_x(x, lt->tanh_c, 0);                      // a NaN / huge argument in the wave
   else
     th = qldpc_tanh_x(x, lt->tanh_c, 1);
@@ -1691,11 +1726,24 @@ __device__ __forceinline__ uint32_t cn_bp_word(const DecodeArgs& a, const qldpc_
   // lane-to-lane prefix chain, without its per-step index arithmetic, selects
   // and final broadcast (BP flooding is VALU-bound)
   const int base = lane & ~7;
-  double P = __shfl(th, base, 64);
+  double P;
+  if constexpr (QLDPC_BP_FOLD) {
+    // every permute issued before the first product: one LDS round trip of
+    // latency instead of DC - 1 in the fold's dependency chain
+    double tv[DC];
 #pragma unroll
-  for (int s = 1; s < DC; ++s) P = P * __shfl(th, base + s, 64);
+    for (int s = 0; s < DC; ++s) tv[s] = __shfl(th, base + s, 64);
+    __builtin_amdgcn_sched_barrier(0);
+    P = tv[0];
+#pragma unroll
+    for (int s = 1; s < DC; ++s) P = P * tv[s];
+  } else {
+    P = __shfl(th, base, 64);
+#pragma unroll
+    for (int s = 1; s < DC; ++s) P = P * __shfl(th, base + s, 64);
+  }
   // parity of the hard decisions of the posteriors this check read (:283-285)
-  const uint64_t hb = ballot(ek && pj < 0.0);
+  const uint64_t hb = ballot_b(ek && pj < 0.0);
   const uint32_t par = (uint32_t)__builtin_popcount((uint32_t)(hb >> (lane & 56)) & 0xffu) & 1u;
   // Every lane computes (a pad lane: th = 1, its results discarded); only
   // the message store is guarded.
@@ -1704,7 +1752,7 @@ __device__ __forceinline__ uint32_t cn_bp_word(const DecodeArgs& a, const qldpc_
   // (a -0 product keeps its sign only through v_div_fixup), tiny or
   // non-finite one divides the general way.
   double th2;
-  if (__builtin_expect(ballot(ek && !(__builtin_fabs(th) > 1e-150 && __builtin_fabs(P) > 1e-150)) != 0, 0))
+  if (__builtin_expect(ballot_b(ek && !(__builtin_fabs(th) > 1e-150 && __builtin_fabs(P) > 1e-150)) != 0, 0))
     th2 = P / th;
   else
     th2 = QLDPC_DIV(P, th);
@@ -1715,7 +1763,7 @@ __device__ __forceinline__ uint32_t cn_bp_word(const DecodeArgs& a, const qldpc_
   // np.arctanh (:259); SVML's rare path (|th2| >= 1, NaN) only when a lane
   // of the wave needs it
   double at;
-  if (__builtin_expect(ballot(ek && !(__builtin_fabs(th2) < 1.0)) != 0, 0))
+  if (__builtin_expect(ballot_b(ek && !(__builtin_fabs(th2) < 1.0)) != 0, 0))
     at = qldpc_atanh_x(th2, lt->atanh_hl, lt->atanh_rcp, 0);
   else
     at = qldpc_atanh_x(th2, lt->atanh_hl, lt->atanh_rcp, 1);
@@ -1726,13 +1774,13 @@ __device__ __forceinline__ uint32_t cn_bp_word(const DecodeArgs& a, const qldpc_
   return valid ? (par ^ synb) : 0u;
 }
 
-template <int DC>
+template <int DC, bool SAT>
 __device__ __forceinline__ uint32_t cn_bp_group(const DecodeArgs& a, const LdsView& g, int c, bool valid,
                                                 int k, int lane, uint32_t synb, const double* post,
                                                 double* c2v, int& fl) {
   const uint32_t tw = g.cn_tab[8 * c + k];                     // (c = 0 for a pad check)
   const uint32_t t = (valid && k < DC) ? tw : 0u;
-  return cn_bp_word<DC>(a, g.lt, t, valid, k, lane, synb, post, c2v, fl);
+  return cn_bp_word<DC, SAT>(a, g.lt, t, valid, k, lane, synb, post, c2v, fl);
 }
 
 // Every graph table in LDS: the flooding BP kernel (VALU-bound), and the
@@ -1818,7 +1866,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
           const int c = c0 + grp;
           const bool valid = c < m;
           const uint32_t sb = valid ? (synw[c >> 5] >> (c & 31)) & 1u : 0u;
-          unsat |= cn_bp_group<DC>(a, g, valid ? c : 0, valid, k, lane, sb, post, c2v, fl);
+          unsat |= cn_bp_group<DC, QLDPC_BP_SAT_F>(a, g, valid ? c : 0, valid, k, lane, sb, post, c2v, fl);
         }
         // the parity pass is the stop test of iteration it-1 (:283-285); its
         // team barrier also orders these c2v writes before the VN reads them
@@ -1866,7 +1914,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
             const bool valid = q < q1;
             const int c = valid ? (int)g.lay_rows[q] : 0;
             const uint32_t sb = valid ? (synw[c >> 5] >> (c & 31)) & 1u : 0u;
-            (void)cn_bp_group<DC>(a, g, c, valid, k, lane, sb, post, c2v, fl);
+            (void)cn_bp_group<DC, QLDPC_BP_SAT>(a, g, c, valid, k, lane, sb, post, c2v, fl);
           }
           __syncthreads();
           // VN over the layer's adjacent variables
@@ -2034,7 +2082,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
             const bool valid = q0 + GP * i + grp < q1;
             const int c = (int)pc[i];
             const uint32_t sb = valid ? (synw[c >> 5] >> (c & 31)) & 1u : 0u;
-            (void)cn_bp_word<DC>(a, lt, pt[i], valid, k, lane, sb, post, c2v, fl);
+            (void)cn_bp_word<DC, QLDPC_BP_SAT>(a, lt, pt[i], valid, k, lane, sb, post, c2v, fl);
           }
         }
         for (int qb = q0 + GP * NPF; qb < q1; qb += GP) {  // layers of more than NPF passes
@@ -2043,7 +2091,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
           const int c = valid ? (int)lrow_g[q] : 0;
           const uint32_t t = (valid && k < DC) ? ltab_g[8 * q + k] : 0u;
           const uint32_t sb = valid ? (synw[c >> 5] >> (c & 31)) & 1u : 0u;
-          (void)cn_bp_word<DC>(a, lt, t, valid, k, lane, sb, post, c2v, fl);
+          (void)cn_bp_word<DC, QLDPC_BP_SAT>(a, lt, t, valid, k, lane, sb, post, c2v, fl);
         }
         rows_pf(l + 1 < nl ? l + 1 : 0);                  // in flight during the VN
         __syncthreads();

@@ -15,7 +15,8 @@
      defined(QLDPC_OSD_WPE) || defined(QLDPC_OSD_PRIO) || defined(QLDPC_VN_PREINFO) ||                \
      defined(QLDPC_ABLATE_ORD) || defined(QLDPC_OSD_DSPLIT) ||                                     \
      defined(QLDPC_OSD_SFEXACT) || defined(QLDPC_MSL_GT) ||                                      \
-     defined(QLDPC_OSD_PAIRS) || defined(QLDPC_MSL_KARGS))
+     defined(QLDPC_OSD_PAIRS) || defined(QLDPC_MSL_KARGS) || defined(QLDPC_BP_SAT) || defined(QLDPC_BP_FOLD) ||                 \
+     defined(QLDPC_BP_SAT_F))
 #error "kernel tuning knobs are for experiment builds: add -DQLDPC_EXPERIMENTS"
 #endif
 
@@ -81,6 +82,18 @@
 #ifndef QLDPC_MSL_GT
 #define QLDPC_MSL_GT 1       // ms_layered_kernel<DC, 1>: row table and filter words in global memory, 8
                              // waves per CU (1: LP118_2 p = 0.1 39.9 -> 36.5 ms per launch), or in LDS (0)
+#endif
+#ifndef QLDPC_BP_SAT
+#define QLDPC_BP_SAT 1       // BP check node: a wave whose every edge has |v2c / 2| >= 19.5 (NumPy's
+                             // tanh = +-1 exactly) takes c2v = +-2 atanh(1 - eps) without the tanh,
+                             // the product, the division and the atanh (0: always the full path)
+#endif
+#ifndef QLDPC_BP_SAT_F
+#define QLDPC_BP_SAT_F 0     // the same in the flooding BP kernel (bp_team_kernel<false, ..>)
+#endif
+#ifndef QLDPC_BP_FOLD
+#define QLDPC_BP_FOLD 0      // BP check node: the group's t values all permuted before np.prod's fold (1)
+                             // or one permute per fold step (0)
 #endif
 #ifndef QLDPC_VN_PREINFO
 #define QLDPC_VN_PREINFO 0     // ms_layered_kernel<DC, 1>: first VN adjacency words read at the layer head

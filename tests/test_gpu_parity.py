@@ -155,6 +155,8 @@ def _channel(Hx, Hz, p, B, seed):
     ("LP118_0", "L", "MS", None, 50, 512),
     ("LP04_0", "L", "MS", 0.08, 50, 1024),        # layered MS, row degree 7
     ("LP118_2", "S", "MS", 0.05, 4, 256),         # serial schedule: 450 one-row layers
+    ("LP118_2", "L", "BP", 0.12, 100, 256),       # many failing decodes: saturated check nodes (|v2c/2| >= 19.5)
+    ("LP118_2", "F", "BP", 0.12, 60, 128),
 ])
 def test_kernel_matches_oracle_batches(dec, code, sched, algo, p, max_iter, B):
     from oracle import oracle

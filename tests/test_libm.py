@@ -95,3 +95,20 @@ def test_special_values(probe):
     a = _run(probe, "va", np.array([0.0, 1.0, -1.0, 1 - 1e-9, 2.0]))
     assert a[0] == 0 and np.isposinf(a[1]) and np.isneginf(a[2]) and np.isnan(a[4])
     assert a[3] == np.arctanh(1 - 1e-9)
+
+
+def test_tanh_saturates_at_bp_threshold(probe):
+    """decoder_kernels.hip's saturated check-node path (kBpTanhSat = 19.5)
+    takes tanh(x) = +-1.0 exactly for every |x| >= 19.5: dense and random
+    arguments over [19.5, 24) (the polynomial interval) and beyond, against
+    the restatement and NumPy; just below, tanh is not yet 1 everywhere."""
+    rng = np.random.default_rng(7)
+    lo = np.nextafter(19.5, 0.0)
+    x = np.concatenate([np.linspace(19.5, 24.0, 2_000_001), rng.uniform(19.5, 24.0, 2_000_000),
+                        rng.uniform(24.0, 1e6, 200_000), [19.5, 24.0, np.nextafter(24.0, 0.0), 1e300]])
+    for s in (1.0, -1.0):
+        got = _run(probe, "vt", s * x)
+        assert np.all(got == s), "restated tanh below 1 past the threshold"
+        assert np.all(np.tanh(s * x) == s), "NumPy's tanh below 1 past the threshold"
+    below = np.linspace(18.0, lo, 100_001)
+    assert np.any(_run(probe, "vt", below) != 1.0)
