@@ -2033,8 +2033,17 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
     for (int i = 0; i < NPF; ++i) {
       const int q = q0 + GP * i + grp;
       const bool v = q < q1;
-      pt[i] = (v && k < DC) ? ltab_g[8 * q + k] : 0u;
-      pc[i] = v ? lrow_g[q] : 0u;
+      if constexpr (QLDPC_BP_ULOAD) {
+        // every lane loads (a pad lane row 0, in bounds): no exec-masked
+        // loads, so the wait counts before the first use stay exact
+        const int qc = v ? q : 0;
+        const uint32_t w = ltab_g[8 * qc + k], r = lrow_g[qc];
+        pt[i] = (v && k < DC) ? w : 0u;
+        pc[i] = v ? r : 0u;
+      } else {
+        pt[i] = (v && k < DC) ? ltab_g[8 * q + k] : 0u;
+        pc[i] = v ? lrow_g[q] : 0u;
+      }
     }
   };
 
@@ -2074,14 +2083,21 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
 #pragma unroll
         for (int i = 0; i < NAF; ++i) {
           const int q = v0 + TS * i + tid;
-          pa[i] = q < v1 ? adj_g[q] : 0u;
+          if constexpr (QLDPC_BP_ULOAD) {
+            const uint32_t w = adj_g[q < v1 ? q : 0];     // unmasked load (slot 0 in bounds)
+            pa[i] = q < v1 ? w : 0u;
+          } else {
+            pa[i] = q < v1 ? adj_g[q] : 0u;
+          }
         }
 #pragma unroll
         for (int i = 0; i < NPF; ++i) {
           if (q0 + GP * i < q1) {
             const bool valid = q0 + GP * i + grp < q1;
             const int c = (int)pc[i];
-            const uint32_t sb = valid ? (synw[c >> 5] >> (c & 31)) & 1u : 0u;
+            // (c = 0 for a pad check: an unmasked in-bounds read)
+            const uint32_t sb = (QLDPC_BP_ULOAD ? (synw[c >> 5] >> (c & 31)) & (valid ? 1u : 0u)
+                                                : (valid ? synw[c >> 5] >> (c & 31) : 0u)) & 1u;
             (void)cn_bp_word<DC, QLDPC_BP_SAT>(a, lt, pt[i], valid, k, lane, sb, post, c2v, fl);
           }
         }

@@ -15,8 +15,8 @@
      defined(QLDPC_OSD_WPE) || defined(QLDPC_OSD_PRIO) || defined(QLDPC_VN_PREINFO) ||                \
      defined(QLDPC_ABLATE_ORD) || defined(QLDPC_OSD_DSPLIT) ||                                     \
      defined(QLDPC_OSD_SFEXACT) || defined(QLDPC_MSL_GT) ||                                      \
-     defined(QLDPC_OSD_PAIRS) || defined(QLDPC_MSL_KARGS) || defined(QLDPC_BP_SAT) || defined(QLDPC_BP_FOLD) ||                 \
-     defined(QLDPC_BP_SAT_F))
+     defined(QLDPC_OSD_PAIRS) || defined(QLDPC_MSL_KARGS) || defined(QLDPC_BP_SAT) ||                \
+     defined(QLDPC_BP_FOLD) || defined(QLDPC_BP_SAT_F) || defined(QLDPC_BP_ULOAD))
 #error "kernel tuning knobs are for experiment builds: add -DQLDPC_EXPERIMENTS"
 #endif
 
@@ -84,15 +84,23 @@
                              // waves per CU (1: LP118_2 p = 0.1 39.9 -> 36.5 ms per launch), or in LDS (0)
 #endif
 #ifndef QLDPC_BP_SAT
-#define QLDPC_BP_SAT 1       // BP check node: a wave whose every edge has |v2c / 2| >= 19.5 (NumPy's
-                             // tanh = +-1 exactly) takes c2v = +-2 atanh(1 - eps) without the tanh,
-                             // the product, the division and the atanh (0: always the full path)
+#define QLDPC_BP_SAT 1       // layered BP check node: a wave whose every edge has |v2c / 2| >= 19.5
+                             // (NumPy's tanh = +-1 exactly) takes c2v = +-2 atanh(1 - eps) without the
+                             // tanh, the product, the division and the atanh (0: always the full path);
+                             // LP118_2 p = 0.1 111.8 -> 107.6 ms per launch (profiles/r05/bp_sat_ab.json)
 #endif
 #ifndef QLDPC_BP_SAT_F
-#define QLDPC_BP_SAT_F 0     // the same in the flooding BP kernel (bp_team_kernel<false, ..>)
+#define QLDPC_BP_SAT_F 0     // the same in the flooding BP kernel (bp_team_kernel<false, ..>): its check
+                             // costs 2.9 % on the fixed-work LP118_0 decode, which never saturates
+#endif
+#ifndef QLDPC_BP_ULOAD
+#define QLDPC_BP_ULOAD 0     // bp_team_lg_kernel: row / adjacency prefetches and syndrome bits read by
+                             // every lane (pad lanes: slot 0) instead of under an exec mask (1: exact wait
+                             // counts, yet LP118_2 p = 0.1 107.5 -> 111.0 ms, profiles/r05/bp_uload_ab.json)
 #endif
 #ifndef QLDPC_BP_FOLD
-#define QLDPC_BP_FOLD 0      // BP check node: the group's t values all permuted before np.prod's fold (1)
+#define QLDPC_BP_FOLD 0      // BP check node: the group's t values all permuted before np.prod's fold (1:
+                             // +2.1 % per LP118_2 p = 0.1 launch, -0.8 % BP-F, profiles/r05/bp_fold_ab.json)
                              // or one permute per fold step (0)
 #endif
 #ifndef QLDPC_VN_PREINFO
