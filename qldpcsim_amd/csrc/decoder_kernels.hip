@@ -1879,8 +1879,10 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
         } else {
           __syncthreads();
         }
+        if constexpr (QLDPC_BP_FVNPRIO != 0) __builtin_amdgcn_s_setprio(QLDPC_BP_FVNPRIO);
         for (int j = tid; j < n; j += TS) post[j] = vn_post<ALGO_BP>(a, g, j, c2v, -1);
         __syncthreads();
+        if constexpr (QLDPC_BP_FVNPRIO != 0) __builtin_amdgcn_s_setprio(0);
         if (it + 1 == a.max_iter) {
           uint32_t un = 0;
           for (int c = tid; c < m; c += TS) {
@@ -1918,6 +1920,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
           }
           __syncthreads();
           // VN over the layer's adjacent variables
+          if constexpr (QLDPC_BP_FVNPRIO != 0) __builtin_amdgcn_s_setprio(QLDPC_BP_FVNPRIO);
           const int v0 = g.adj_ptr[l], v1 = g.adj_ptr[l + 1];
           uint32_t acc = 0;
           for (int q = v0 + tid; q < v1; q += TS) {
@@ -1930,6 +1933,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
           const uint32_t wacc = wave_xor(acc);
           if (lane == 0) fsl[wid] = wacc;
           __syncthreads();
+          if constexpr (QLDPC_BP_FVNPRIO != 0) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
           for (int w = 0; w < W; ++w) F ^= fsl[w];
           if (F == B) {                                   // team-uniform
@@ -2110,6 +2114,10 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
           (void)cn_bp_word<DC, QLDPC_BP_SAT>(a, lt, t, valid, k, lane, sb, post, c2v, fl);
         }
         rows_pf(l + 1 < nl ? l + 1 : 0);                  // in flight during the VN
+        // the team's variable nodes ahead of other teams' check nodes on the
+        // SIMD: a layer's VN is short and every wave of the team waits for it
+        // at the next barrier
+        if constexpr (QLDPC_BP_VNPRIO != 0) __builtin_amdgcn_s_setprio(QLDPC_BP_VNPRIO);
         __syncthreads();
         uint32_t acc = 0;                                 // VN over the layer's adjacent variables
         auto vn = [&](uint32_t info) {
@@ -2127,6 +2135,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
         const uint32_t wacc = wave_xor(acc);
         if (lane == 0) fsl[wid] = wacc;
         __syncthreads();
+        if constexpr (QLDPC_BP_VNPRIO != 0) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
         for (int w = 0; w < W; ++w) F ^= fsl[w];
         if (F == B) {                                     // team-uniform

@@ -16,7 +16,8 @@
      defined(QLDPC_ABLATE_ORD) || defined(QLDPC_OSD_DSPLIT) ||                                     \
      defined(QLDPC_OSD_SFEXACT) || defined(QLDPC_MSL_GT) ||                                      \
      defined(QLDPC_OSD_PAIRS) || defined(QLDPC_MSL_KARGS) || defined(QLDPC_BP_SAT) ||                \
-     defined(QLDPC_BP_FOLD) || defined(QLDPC_BP_SAT_F) || defined(QLDPC_BP_ULOAD))
+     defined(QLDPC_BP_FOLD) || defined(QLDPC_BP_SAT_F) || defined(QLDPC_BP_ULOAD) ||\
+     defined(QLDPC_BP_VNPRIO) || defined(QLDPC_BP_FVNPRIO))
 #error "kernel tuning knobs are for experiment builds: add -DQLDPC_EXPERIMENTS"
 #endif
 
@@ -97,6 +98,16 @@
 #define QLDPC_BP_ULOAD 0     // bp_team_lg_kernel: row / adjacency prefetches and syndrome bits read by
                              // every lane (pad lanes: slot 0) instead of under an exec mask (1: exact wait
                              // counts, yet LP118_2 p = 0.1 107.5 -> 111.0 ms, profiles/r05/bp_uload_ab.json)
+#endif
+#ifndef QLDPC_BP_VNPRIO
+#define QLDPC_BP_VNPRIO 2    // bp_team_lg_kernel: s_setprio of a layer's variable-node phase (0: none);
+                             // 2: LP118_2 p = 0.1 107.2 -> 103.8 ms per launch (the check-node phase at
+                             // priority 2 instead: 106.3 ms), profiles/r05/bp_prio_ab.json; levels 1 / 3
+                             // within 0.7 % of 2 (bp_prio_levels_ab.json)
+#endif
+#ifndef QLDPC_BP_FVNPRIO
+#define QLDPC_BP_FVNPRIO 0   // the same for bp_team_kernel (flooding and the all-LDS layered fallback);
+                             // 2: LP118_0 BP-F fixed work 76.82 -> 76.73 ms (within noise), not kept
 #endif
 #ifndef QLDPC_BP_FOLD
 #define QLDPC_BP_FOLD 0      // BP check node: the group's t values all permuted before np.prod's fold (1:
