@@ -1692,6 +1692,8 @@ __device__ __forceinline__ uint32_t cn_bp_word(const DecodeArgs& a, const qldpc_
   // 0, in bounds) and the pad lanes' values are replaced by selects — no
   // exec-masked branches around the loads and the tanh
   if (ballot_b(valid) == 0) return 0u;
+  constexpr int CP = SAT ? QLDPC_BP_CNPRIO : 0;          // experiment: check-node phase priorities
+  if constexpr (CP == 1 || CP == 2) __builtin_amdgcn_s_setprio(1);
   const int j = (int)((t & 0xffffu) >> 3), p = (int)(t >> 18);
   const double pjr = post[j];
   const double x = (pjr - c2v[p]) / 2.0;                      // v2c (:269)
@@ -1711,6 +1713,7 @@ __device__ __forceinline__ uint32_t cn_bp_word(const DecodeArgs& a, const qldpc_
     if (ek) c2v[p] = neg ? -csat : csat;
     const uint64_t hb = ballot_b(ek && pjr < 0.0);
     const uint32_t par = (uint32_t)__builtin_popcount((uint32_t)(hb >> (lane & 56)) & 0xffu) & 1u;
+    if constexpr (CP == 1 || CP == 2) __builtin_amdgcn_s_setprio(0);
     return valid ? (par ^ synb) : 0u;
   }
   double th;                                                  // np.tanh (:254)
@@ -1719,6 +1722,7 @@ __device__ __forceinline__ uint32_t cn_bp_word(const DecodeArgs& a, const qldpc_
   else
     th = qldpc_tanh_x(x, lt->tanh_c, 1);
   th = ek ? th : 1.0;
+  if constexpr (CP == 1) __builtin_amdgcn_s_setprio(0);
   const double pj = ek ? pjr : 0.0;
   // np.prod: sequential left fold over the check's edges in ascending variable
   // order, ((t_0 t_1) t_2) ..., formed redundantly by every lane of the group
@@ -1760,6 +1764,8 @@ __device__ __forceinline__ uint32_t cn_bp_word(const DecodeArgs& a, const qldpc_
   // is copysign(|th2| - eps, th2) (round-to-nearest is symmetric in sign;
   // a NaN compares false and stays)
   th2 = (__builtin_fabs(th2) >= 1.0 - a.eps) ? __builtin_copysign(__builtin_fabs(th2) - a.eps, th2) : th2;
+  if constexpr (CP == 2) __builtin_amdgcn_s_setprio(0);
+  if constexpr (CP == 3) __builtin_amdgcn_s_setprio(1);
   // np.arctanh (:259); SVML's rare path (|th2| >= 1, NaN) only when a lane
   // of the wave needs it
   double at;
@@ -1771,6 +1777,7 @@ __device__ __forceinline__ uint32_t cn_bp_word(const DecodeArgs& a, const qldpc_
   if (synb) val = -val;                                   // (:260-261)
   if (ek && (th == 0.0 || !__builtin_isfinite(val))) fl |= FLAG_NONFINITE;
   if (ek) c2v[p] = val;
+  if constexpr (CP == 3) __builtin_amdgcn_s_setprio(0);
   return valid ? (par ^ synb) : 0u;
 }
 
@@ -2135,7 +2142,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
         const uint32_t wacc = wave_xor(acc);
         if (lane == 0) fsl[wid] = wacc;
         __syncthreads();
-        if constexpr (QLDPC_BP_VNPRIO != 0) __builtin_amdgcn_s_setprio(0);
+        if constexpr (QLDPC_BP_VNPRIO != 0) __builtin_amdgcn_s_setprio(QLDPC_BP_LHPRIO);
 #pragma unroll
         for (int w = 0; w < W; ++w) F ^= fsl[w];
         if (F == B) {                                     // team-uniform

@@ -17,7 +17,8 @@
      defined(QLDPC_OSD_SFEXACT) || defined(QLDPC_MSL_GT) ||                                      \
      defined(QLDPC_OSD_PAIRS) || defined(QLDPC_MSL_KARGS) || defined(QLDPC_BP_SAT) ||                \
      defined(QLDPC_BP_FOLD) || defined(QLDPC_BP_SAT_F) || defined(QLDPC_BP_ULOAD) ||\
-     defined(QLDPC_BP_VNPRIO) || defined(QLDPC_BP_FVNPRIO))
+     defined(QLDPC_BP_VNPRIO) || defined(QLDPC_BP_FVNPRIO) ||\
+     defined(QLDPC_BP_CNPRIO) || defined(QLDPC_BP_LHPRIO))
 #error "kernel tuning knobs are for experiment builds: add -DQLDPC_EXPERIMENTS"
 #endif
 
@@ -104,6 +105,15 @@
                              // 2: LP118_2 p = 0.1 107.2 -> 103.8 ms per launch (the check-node phase at
                              // priority 2 instead: 106.3 ms), profiles/r05/bp_prio_ab.json; levels 1 / 3
                              // within 0.7 % of 2 (bp_prio_levels_ab.json)
+#endif
+#ifndef QLDPC_BP_CNPRIO
+#define QLDPC_BP_CNPRIO 2    // layered BP check nodes at priority 1 from entry to the tanh (1), to the
+                             // division (2), or from the division to the store (3); 0: none. LP118_2
+                             // p = 0.1 103.9 ms per launch -> 103.3 / 102.1 / 106.5 (bp_cnprio_ab.json)
+#endif
+#ifndef QLDPC_BP_LHPRIO
+#define QLDPC_BP_LHPRIO 1    // bp_team_lg_kernel: priority of the layer head (stop test, prefetch issue);
+                             // 1: 102.1 -> 101.4 ms per LP118_2 p = 0.1 launch (bp_lhprio_ab.json)
 #endif
 #ifndef QLDPC_BP_FVNPRIO
 #define QLDPC_BP_FVNPRIO 0   // the same for bp_team_kernel (flooding and the all-LDS layered fallback);
