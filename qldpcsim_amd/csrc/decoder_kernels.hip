@@ -1589,7 +1589,11 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
         }
         if constexpr ((QLDPC_ABLATE_L & 1) != 0) {
         } else if constexpr (G != 0) {
+          if constexpr (QLDPC_MSL_PRIO == 1) __builtin_amdgcn_s_setprio(1);
+          if constexpr (QLDPC_MSL_PRIO == 2) __builtin_amdgcn_s_setprio(0);
           cn_layer<DC, G, G == 1>(a, ltab, lrow, synw, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl);
+          if constexpr (QLDPC_MSL_PRIO == 1) __builtin_amdgcn_s_setprio(0);
+          if constexpr (QLDPC_MSL_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         } else {
           // lanes per check chosen per layer by the host (bits 5-6 of adj_dmax)
           switch (dsel >> 5) {
@@ -1692,7 +1696,7 @@ __device__ __forceinline__ uint32_t cn_bp_word(const DecodeArgs& a, const qldpc_
   // 0, in bounds) and the pad lanes' values are replaced by selects — no
   // exec-masked branches around the loads and the tanh
   if (ballot_b(valid) == 0) return 0u;
-  constexpr int CP = SAT ? QLDPC_BP_CNPRIO : 0;          // experiment: check-node phase priorities
+  constexpr int CP = SAT ? QLDPC_BP_CNPRIO : QLDPC_BP_FCNPRIO;   // check-node phase priorities
   if constexpr (CP == 1 || CP == 2) __builtin_amdgcn_s_setprio(1);
   const int j = (int)((t & 0xffffu) >> 3), p = (int)(t >> 18);
   const double pjr = post[j];

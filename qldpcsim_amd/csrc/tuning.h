@@ -18,7 +18,8 @@
      defined(QLDPC_OSD_PAIRS) || defined(QLDPC_MSL_KARGS) || defined(QLDPC_BP_SAT) ||                \
      defined(QLDPC_BP_FOLD) || defined(QLDPC_BP_SAT_F) || defined(QLDPC_BP_ULOAD) ||\
      defined(QLDPC_BP_VNPRIO) || defined(QLDPC_BP_FVNPRIO) ||\
-     defined(QLDPC_BP_CNPRIO) || defined(QLDPC_BP_LHPRIO))
+     defined(QLDPC_BP_CNPRIO) || defined(QLDPC_BP_LHPRIO) ||\
+     defined(QLDPC_BP_FCNPRIO) || defined(QLDPC_MSL_PRIO))
 #error "kernel tuning knobs are for experiment builds: add -DQLDPC_EXPERIMENTS"
 #endif
 
@@ -110,6 +111,14 @@
 #define QLDPC_BP_CNPRIO 2    // layered BP check nodes at priority 1 from entry to the tanh (1), to the
                              // division (2), or from the division to the store (3); 0: none. LP118_2
                              // p = 0.1 103.9 ms per launch -> 103.3 / 102.1 / 106.5 (bp_cnprio_ab.json)
+#endif
+#ifndef QLDPC_BP_FCNPRIO
+#define QLDPC_BP_FCNPRIO 2   // the same modes for the flooding BP kernel's check nodes; 2: LP118_0 BP-F
+                             // fixed work 76.9 -> 73.4 ms per launch (profiles/r05/prio_msl_bpf_ab.json)
+#endif
+#ifndef QLDPC_MSL_PRIO
+#define QLDPC_MSL_PRIO 1     // ms_layered_kernel: check nodes at priority 1 (1) or variable nodes at 1 (2);
+                             // LP118_2 p = 0.1 35.05 -> 34.84 / 35.58 ms per launch (prio_msl_bpf_ab.json)
 #endif
 #ifndef QLDPC_BP_LHPRIO
 #define QLDPC_BP_LHPRIO 1    // bp_team_lg_kernel: priority of the layer head (stop test, prefetch issue);
