@@ -564,6 +564,7 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
   }
   QLDPC_TICK(0);                                      // setup
   for (int w = 0; w < NW && 64 * w < n && !done; ++w) {   // done: uniform, re-read per block
+    if constexpr (QLDPC_OSD_APRIO != 0) __builtin_amdgcn_s_setprio(QLDPC_OSD_APRIO);
 #pragma unroll
     for (int h = 0; h < RT; ++h)                      // A
       if (own[h]) {
@@ -575,6 +576,7 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
       }
     __syncthreads();
     QLDPC_TICK(1);
+    if constexpr (QLDPC_OSD_APRIO != 0) __builtin_amdgcn_s_setprio(0);
     if (wave == engine) {                             // B
       // The engine is its shot's critical path while the SIMD also runs
       // other shots' phase-D waves: raised priority lets it issue first.

@@ -19,7 +19,7 @@
      defined(QLDPC_BP_FOLD) || defined(QLDPC_BP_SAT_F) || defined(QLDPC_BP_ULOAD) ||\
      defined(QLDPC_BP_VNPRIO) || defined(QLDPC_BP_FVNPRIO) ||\
      defined(QLDPC_BP_CNPRIO) || defined(QLDPC_BP_LHPRIO) ||\
-     defined(QLDPC_BP_FCNPRIO) || defined(QLDPC_MSL_PRIO))
+     defined(QLDPC_BP_FCNPRIO) || defined(QLDPC_MSL_PRIO) || defined(QLDPC_OSD_APRIO))
 #error "kernel tuning knobs are for experiment builds: add -DQLDPC_EXPERIMENTS"
 #endif
 
@@ -62,6 +62,11 @@
 #ifndef QLDPC_OSD_PRIO
 #define QLDPC_OSD_PRIO 3     // osd_block_kernel: s_setprio of the engine wave during phase B (0: none;
                              // 1 and 3 both -3.3 % per launch, profiles/r04am/)
+#endif
+#ifndef QLDPC_OSD_APRIO
+#define QLDPC_OSD_APRIO 0    // osd_block_kernel: phase A (the block's row words staged for the engine) at
+                             // this priority (0: none); 2: 22.37 -> 22.41 ms per 68,301 shots, not kept
+                             // (profiles/r05/osd_aprio_ab.jsonl)
 #endif
 #ifndef QLDPC_OSD_DSPLIT
 #define QLDPC_OSD_DSPLIT 12  // osd_block_kernel phase D: pivot-row words read in two batches when more
@@ -114,7 +119,9 @@
 #endif
 #ifndef QLDPC_BP_FCNPRIO
 #define QLDPC_BP_FCNPRIO 2   // the same modes for the flooding BP kernel's check nodes; 2: LP118_0 BP-F
-                             // fixed work 76.9 -> 73.4 ms per launch (profiles/r05/prio_msl_bpf_ab.json)
+                             // fixed work 76.9 -> 73.4 ms per launch (profiles/r05/prio_msl_bpf_ab.json;
+                             // 78.5 -> 76.7 on a slower box, round5_ab_start_vs_head.json); mode 1: +1.6 %,
+                             // with FVNPRIO 2: within noise (bpf_prio_modes_ab.json)
 #endif
 #ifndef QLDPC_MSL_PRIO
 #define QLDPC_MSL_PRIO 1     // ms_layered_kernel: check nodes at priority 1 (1) or variable nodes at 1 (2);
