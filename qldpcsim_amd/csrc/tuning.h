@@ -129,7 +129,8 @@
 #endif
 #ifndef QLDPC_BP_LHPRIO
 #define QLDPC_BP_LHPRIO 1    // bp_team_lg_kernel: priority of the layer head (stop test, prefetch issue);
-                             // 1: 102.1 -> 101.4 ms per LP118_2 p = 0.1 launch (bp_lhprio_ab.json)
+                             // 1: 102.1 -> 101.4 ms per LP118_2 p = 0.1 launch (bp_lhprio_ab.json); 2, or
+                             // 3 with the VN at 3: within 0.1 % (bp_lhprio_levels_ab.json)
 #endif
 #ifndef QLDPC_BP_FVNPRIO
 #define QLDPC_BP_FVNPRIO 0   // the same for bp_team_kernel (flooding and the all-LDS layered fallback);

@@ -16,8 +16,14 @@ def _args(code="LP118_0", sched="L"):
 
 
 def test_op_is_registered_and_infers_shapes_on_meta():
-    # registered from C++ (torch_ops.cpp, TORCH_LIBRARY) by the in-tree library
-    assert ops.TORCH_OPS_PATH.endswith("qldpcsim_amd/_build/libqldpc_torch.so")
+    # registered from C++ (torch_ops.cpp, TORCH_LIBRARY) by the library built
+    # beside the decoder library this process loaded (in-tree by default,
+    # QLDPC_LIB's directory for an out-of-tree build)
+    import os
+    from qldpcsim_amd import _lib
+    assert ops.TORCH_OPS_PATH == os.path.join(os.path.dirname(_lib.LIB_PATH), "libqldpc_torch.so")
+    if "QLDPC_LIB" not in os.environ:
+        assert ops.TORCH_OPS_PATH.endswith(os.path.join("qldpcsim_amd", "_build", "libqldpc_torch.so"))
     sch = str(torch.ops.qldpc.decode.default._schema)
     assert sch.startswith("qldpc::decode(Tensor syndromes, Tensor H, Tensor layer_ptr, Tensor layer_rows")
     Hz, H, lp, lr = _args()
