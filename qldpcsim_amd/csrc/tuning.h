@@ -138,8 +138,9 @@
 #endif
 #ifndef QLDPC_BP_FOLD
 #define QLDPC_BP_FOLD 0      // BP check node: the group's t values all permuted before np.prod's fold (1:
-                             // +2.1 % per LP118_2 p = 0.1 launch, -0.8 % BP-F, profiles/r05/bp_fold_ab.json)
-                             // or one permute per fold step (0)
+                             // +2.1 % per LP118_2 p = 0.1 launch, -0.8 % BP-F, profiles/r05/bp_fold_ab.json;
+                             // with the phase priorities +4.3 % / +0.9 %, bp_fold_prio_ab.json) or one
+                             // permute per fold step (0)
 #endif
 #ifndef QLDPC_VN_PREINFO
 #define QLDPC_VN_PREINFO 0     // ms_layered_kernel<DC, 1>: first VN adjacency words read at the layer head
