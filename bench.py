@@ -82,9 +82,12 @@ def parse(argv=None):
     ap.add_argument("--worklog", default=None,
                     help="write per-launch work (kernel, half-shots, iterations) as JSON (profiling)")
     ap.add_argument("--sim-legs", default="3,4",
-                    help="end-to-end simulate_p legs after the headline, comma-separated BASELINE.json "
-                         "config indices (3: LP118_2 MS-L + OSD-0, 4: LP118_2 BP-L; p = 0.1), '' for none")
-    ap.add_argument("--sim-shots", type=int, default=1 << 20, help="shots per rank of each simulate_p leg")
+                    help="end-to-end legs after the headline, comma-separated BASELINE.json config indices "
+                         "(3: LP118_2 MS-L + OSD-0 at p = 0.1, strong and per-rank; 4: LP118_2 BP-L, the "
+                         "p-sweep [0.01, 0.02, 0.05, 0.1] through simulate), '' for none")
+    ap.add_argument("--sim-shots", type=int, default=1 << 20,
+                    help="shots of the configs[3] job in total (strong; the per-rank leg: per rank) and of "
+                         "each configs[4] p-point in total")
     return ap.parse_args(argv)
 
 
@@ -385,66 +388,147 @@ def cpu_baselines(args):
 
 
 # ---------------------------------------------------------------------------
-# end-to-end simulate_p legs (BASELINE.json configs[3] / configs[4])
+# end-to-end legs: BASELINE.json configs[3] / configs[4] as they are stated
 # ---------------------------------------------------------------------------
 SIM_LEGS = {
     3: dict(code="LP118_2", decType="MS", decSchedule="L", OSDorder=0, decIterations=50, p=0.1,
-            config="BASELINE.json configs[3]: LP118_2, MS layered + OSD-0, 1e6 shots sharded across GPUs"),
-    4: dict(code="LP118_2", decType="BP", decSchedule="L", OSDorder=4, decIterations=100, p=0.1,
+            config="BASELINE.json configs[3]: LP118_2, MS layered + OSD-0, a fixed total of shots sharded "
+                   "across the GPUs (strong scaling), p = 0.1"),
+    4: dict(code="LP118_2", decType="BP", decSchedule="L", OSDorder=4, decIterations=100,
+            p=[0.01, 0.02, 0.05, 0.1],
             config="BASELINE.json configs[4]: LP118_2, BP layered + OSD order 4 (simulate never passes "
-                   "OSDorder to BP_decoder, simulator.py:281-282), p = 0.1 point of the sweep"),
+                   "OSDorder to BP_decoder, simulator.py:281-282), the p-sweep [0.01, 0.02, 0.05, 0.1] "
+                   "through simulate's own p loop (simulator.py:335), a fixed total of shots per p-point "
+                   "sharded across the GPUs"),
 }
 
 
-def sim_leg(idx, shots_per_rank, dist=None, warmup_shots=1 << 18, sampler=None):
-    """One BASELINE config end to end through the drop-in simulate_p
-    (reference simulator.py:167-315): device sampler, decode, OSD, device
-    counters; each rank decodes its contiguous share of world x shots_per_rank
-    shots and simulate_p all-reduces the six counters (its only collective).
-    Timed between barriers + device syncs, max over ranks."""
+def _sync(dist):
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+    except ImportError:
+        pass
+    if dist is not None:
+        dist.barrier()
+
+
+def _gather(dist, world, me):
+    if dist is None or world == 1:
+        return [me]
+    ranks = [None] * world
+    dist.all_gather_object(ranks, me)
+    return ranks
+
+
+def sim_leg(idx, shots, dist=None, warmup_shots=1 << 18, sampler=None, per_rank=False):
+    """configs[3] end to end through the drop-in simulate_p (reference
+    simulator.py:167-315): device sampler, decode, OSD, device counters. The
+    job is `shots` shots in total, each rank its contiguous share (strong
+    scaling, BASELINE's "1e6 shots sharded across 8 MI355X"); per_rank=True
+    gives every rank `shots` of its own instead (weak scaling). simulate_p
+    all-reduces the six counters (its only collective). Timed between
+    barriers + device syncs, max over ranks."""
     from qldpcsim_amd import codes, decoders, hostcores, simulator
     leg = SIM_LEGS[idx]
     world = dist.get_world_size() if dist is not None else 1
+    total = world * shots if per_rank else shots
     Hx, Hz = codes.load_code(leg["code"])
     kw = dict(decType=leg["decType"], decIterations=leg["decIterations"], decSchedule=leg["decSchedule"],
               OSDorder=leg["OSDorder"], verbose=False, sampler=sampler)
-
-    def sync():
-        try:
-            import torch
-            if torch.cuda.is_available():
-                torch.cuda.synchronize()
-        except ImportError:
-            pass
-        if dist is not None:
-            dist.barrier()
     if warmup_shots:
-        simulator.simulate_p(Hx, Hz, leg["p"], shots=world * min(warmup_shots, shots_per_rank), rngSeed=2, **kw)
+        simulator.simulate_p(Hx, Hz, leg["p"], shots=world * min(warmup_shots, max(1, total // world)),
+                             rngSeed=2, **kw)
     decoders.reset_osd_stats()
-    sync()
+    _sync(dist)
     t0 = time.perf_counter()
-    r = simulator.simulate_p(Hx, Hz, leg["p"], shots=world * shots_per_rank, rngSeed=1, **kw)
-    sync()
+    r = simulator.simulate_p(Hx, Hz, leg["p"], shots=total, rngSeed=1, **kw)
+    _sync(dist)
     mine = time.perf_counter() - t0
     st = dict(decoders.OSD_STATS)
-    me = {"elapsed_s": mine, "shots_per_s": shots_per_rank / mine, "host_cores": hostcores.rank_cores(),
+    rank = dist.get_rank() if dist is not None else 0
+    my_shots = total // world + (1 if rank < total % world else 0)
+    me = {"shots": my_shots, "elapsed_s": mine, "shots_per_s": my_shots / mine, "host_cores": hostcores.rank_cores(),
           "osd_shots": st["osd_shots"], "host_order_shots": st["host_order_shots"]}
-    ranks = [me]
-    if dist is not None and world > 1:
-        ranks = [None] * world
-        dist.all_gather_object(ranks, me)
+    ranks = _gather(dist, world, me)
     el = max(x["elapsed_s"] for x in ranks)
-    shots = world * shots_per_rank
     osd = sum(x["osd_shots"] for x in ranks)
     host = sum(x["host_order_shots"] for x in ranks)
     return {"config": leg["config"], "code": leg["code"], "decType": leg["decType"],
             "decSchedule": leg["decSchedule"], "OSDorder": leg["OSDorder"], "decIterations": leg["decIterations"],
-            "p": leg["p"], "shots": shots, "n_ranks": world, "value": shots / el, "unit": "shots/s",
-            "elapsed_s": el, "per_rank": ranks, "osd_shots": osd, "host_order_shots": host,
-            "host_order_share": host / osd if osd else 0.0,
-            "qBLER": 1.0 - (r["decSuccessExact"] + r["decSuccessDegen"]) / shots, "counters": r,
+            "p": leg["p"], "scaling": "weak" if per_rank else "strong", "shots": total, "n_ranks": world,
+            "value": total / el, "unit": "shots/s", "elapsed_s": el, "per_rank": ranks, "osd_shots": osd,
+            "host_order_shots": host, "host_order_share": host / osd if osd else 0.0,
+            "qBLER": 1.0 - (r["decSuccessExact"] + r["decSuccessDegen"]) / total, "counters": r,
             "timing": "simulate_p between barrier + device sync, max over ranks; counters all-reduced "
                       "inside simulate_p (one all_reduce(SUM) of six int64)"}
+
+
+def sim_sweep_leg(idx, shots, dist=None, warmup_shots=1 << 16, sampler=None):
+    """configs[4]'s qBLER curve end to end through the drop-in simulate
+    (reference simulator.py:319-347) and its own p loop (:335): `shots` shots
+    per p-point in total, each rank its share, the six counters all-reduced
+    per point inside simulate_p. The whole sweep is timed between barriers +
+    device syncs (max over ranks); each point by simulate's on_point hook
+    (its all-reduce ends every point on all ranks together; max over ranks)."""
+    import contextlib
+    import tempfile
+    from qldpcsim_amd import codes, hostcores, simulator
+    leg = SIM_LEGS[idx]
+    world = dist.get_world_size() if dist is not None else 1
+    Hx, Hz = codes.load_code(leg["code"])
+    tmp = tempfile.mkdtemp(prefix="qldpc_bench_")
+    fx, fz = os.path.join(tmp, "Hx.npy"), os.path.join(tmp, "Hz.npy")
+    np.save(fx, Hx)
+    np.save(fz, Hz)
+    kw = dict(decType=leg["decType"], decIterations=leg["decIterations"], decSchedule=leg["decSchedule"],
+              OSDorder=leg["OSDorder"], verbose=False, sampler=sampler)
+    if warmup_shots:
+        simulator.simulate_p(Hx, Hz, max(leg["p"]), shots=world * warmup_shots, rngSeed=2, **kw)
+    points = []
+    _sync(dist)
+    t0 = time.perf_counter()
+    with contextlib.redirect_stdout(sys.stderr):         # simulate's results table: not bench's JSON line
+        res = simulator.simulate(fx, fz, leg["p"], shots=shots, rngSeed=1, return_results=True,
+                                 on_point=lambda pT, r, sec: points.append(sec), **kw)
+    _sync(dist)
+    mine = time.perf_counter() - t0
+    for f in (fx, fz):
+        os.remove(f)
+    os.rmdir(tmp)
+    ranks = _gather(dist, world, {"elapsed_s": mine, "points_s": points, "host_cores": hostcores.rank_cores()})
+    el = max(x["elapsed_s"] for x in ranks)
+    curve = []
+    for i, (pT, r) in enumerate(zip(leg["p"], res)):
+        sec = max(x["points_s"][i] for x in ranks)
+        curve.append({"p": pT, "shots": shots, "elapsed_s": sec, "value": shots / sec, "unit": "shots/s",
+                      "qBLER": 1.0 - (r["decSuccessExact"] + r["decSuccessDegen"]) / shots, "counters": r})
+    return {"config": leg["config"], "code": leg["code"], "decType": leg["decType"],
+            "decSchedule": leg["decSchedule"], "OSDorder": leg["OSDorder"], "decIterations": leg["decIterations"],
+            "p": leg["p"], "scaling": "strong", "shots_per_point": shots, "n_ranks": world,
+            "value": shots * len(leg["p"]) / el, "unit": "shots/s (whole sweep)", "elapsed_s": el,
+            "curve": curve, "per_rank": [{"elapsed_s": x["elapsed_s"], "points_s": x["points_s"],
+                                          "host_cores": x["host_cores"]} for x in ranks],
+            "timing": "simulate(p=[...]) between barrier + device sync, max over ranks; per point: "
+                      "simulate's on_point hook, max over ranks; counters all-reduced per point"}
+
+
+def sim_legs(args, dist, world):
+    """The end-to-end legs bench.py runs after the headline (--sim-legs)."""
+    legs = [int(x) for x in args.sim_legs.split(",") if x.strip()]
+    out = {}
+    if 3 in legs:
+        strong = sim_leg(3, args.sim_shots, dist)
+        if world == 1:
+            weak = dict(strong, scaling="weak", note="at one GPU the per-rank job is the whole job: "
+                                                     "the same run as the strong leg")
+        else:
+            weak = sim_leg(3, args.sim_shots, dist, per_rank=True)
+        out["configs3"] = dict(strong, weak_per_rank=weak)
+    if 4 in legs:
+        out["configs4"] = sim_sweep_leg(4, args.sim_shots, dist)
+    return out
 
 
 # ---------------------------------------------------------------------------
@@ -604,12 +688,12 @@ def run_rank(args, rank, world, local):
                            "no data-path collective",
         },
         "roofline": roof,
+        "parity_pin": {k: v for k, v in decoders.parity_pins().items()},
     }
     if hbm_leg is not None:
         out["hbm_streaming"] = hbm_leg
-    legs = [int(x) for x in args.sim_legs.split(",") if x.strip()]
-    if legs and not args.worklog:
-        out["simulate"] = [sim_leg(i, args.sim_shots, dist if world > 1 else None) for i in legs]
+    if args.sim_legs.strip() and not args.worklog:
+        out["simulate"] = sim_legs(args, dist if world > 1 else None, world)
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if rank == 0:

@@ -205,6 +205,18 @@ int qldpc_np_argsort_host(const double *h_key, int n, int32_t *h_perm);
  * np.exp alone (SVML exp8_ha restated, |x| < 707). */
 void qldpc_osd_keys_host(const double *h_post, int64_t count, double *h_key, int exp_only);
 
+/* The restated NumPy libm (include/qldpc_libm.h: the code the BP kernels and
+ * the priors run), element-wise on the host: y[i] = f(x[i]) with f = np.tanh
+ * (QLDPC_LIBM_TANH, decoders.py:254), np.arctanh (QLDPC_LIBM_ATANH, :259),
+ * np.log (QLDPC_LIBM_LOG, :147, :232) or np.exp (QLDPC_LIBM_EXP, :322).
+ * Replaces no reference interface: it lets a caller check at run time that
+ * the NumPy it runs computes the same bits (decoders.numpy_libm_pinned). */
+#define QLDPC_LIBM_TANH 0
+#define QLDPC_LIBM_ATANH 1
+#define QLDPC_LIBM_LOG 2
+#define QLDPC_LIBM_EXP 3
+int qldpc_libm_eval_host(int fn, const double *h_x, int64_t count, double *h_y);
+
 /* qldpc_osd_device with the order computed on the device
  * (qldpc_osd_order_device into the caller's workspaces d_perm / d_tiepos):
  * a shot whose order the device leaves to NumPy (tiepos -1) gets d_status 2

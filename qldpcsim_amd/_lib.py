@@ -28,7 +28,7 @@ EXPORTS = (
     "qldpc_decode_launch_info",
     "qldpc_osd_decode", "qldpc_osd_decode_batch", "qldpc_osd_device", "qldpc_osd_order_device",
     "qldpc_osd_device_ordered", "qldpc_osd_device_ordered_ex", "qldpc_cpython_setdiff_first",
-    "qldpc_osd_order_host", "qldpc_np_argsort_host", "qldpc_osd_keys_host",
+    "qldpc_osd_order_host", "qldpc_np_argsort_host", "qldpc_osd_keys_host", "qldpc_libm_eval_host",
     "qldpc_channel_thresholds", "qldpc_channel_sample", "qldpc_channel_sample_ex", "qldpc_count_outcomes",
     "qldpc_count_outcomes_ex",
     "qldpc_timing_enable", "qldpc_timing_reset", "qldpc_timing_read",
@@ -82,6 +82,7 @@ def _load():
         "qldpc_osd_order_host": ([P, I64, I, P, P, I], I),
         "qldpc_np_argsort_host": ([P, I, P], I),
         "qldpc_osd_keys_host": ([P, I64, P, I], None),
+        "qldpc_libm_eval_host": ([I, P, I64, P], I),
         "qldpc_channel_thresholds": ([D, P, P, P], I),
         "qldpc_channel_sample": ([P, P, D, ctypes.c_uint64, ctypes.c_uint64, I64, P, P, P, P, P], I),
         "qldpc_channel_sample_ex": ([P, P, D, ctypes.c_uint64, ctypes.c_uint64, I64, P, P, P, P, I, P], I),

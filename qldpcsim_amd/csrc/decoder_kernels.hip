@@ -1341,10 +1341,9 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
 // QLDPC_VN_H (4: LP118_2's 240 / 480 in one / two passes instead of two / four,
 // -6.5 % per launch), smaller ones 2 (a 4-wide pass over <= 128 variables
 // idles half its lanes: LP118_0 +4 %)
-template <int K, int H, bool PRE>
+template <int K, int H>
 __device__ __forceinline__ uint32_t vn_layer(const uint32_t* adj_info, const uint32_t* avar, float* colS,
-                                             const float* c2v, int v0, int v1, int lane, float thr,
-                                             const uint32_t* pre) {
+                                             const float* c2v, int v0, int v1, int lane, float thr) {
   uint32_t acc = 0;
   auto trip = [&](int qb, const uint32_t (&info)[H]) {
     bool in[H];
@@ -1384,19 +1383,7 @@ __device__ __forceinline__ uint32_t vn_layer(const uint32_t* adj_info, const uin
       acc ^= flip ? av[h] : 0u;
     }
   };
-  int qb = v0;
-  if constexpr (PRE) {
-    // first trip: adjacency words read at the layer head (vn_preinfo)
-    static_assert(H <= 4, "vn_preinfo reads 4 words per lane");
-    if (v0 < v1) {                                          // (uniform)
-      uint32_t info[H];
-#pragma unroll
-      for (int h = 0; h < H; ++h) info[h] = pre[h];
-      trip(qb, info);
-      qb += 64 * H;
-    }
-  }
-  for (; qb < v1; qb += 64 * H) {
+  for (int qb = v0; qb < v1; qb += 64 * H) {
     uint32_t info[H];
 #pragma unroll
     for (int h = 0; h < H; ++h) {
@@ -1406,15 +1393,6 @@ __device__ __forceinline__ uint32_t vn_layer(const uint32_t* adj_info, const uin
     trip(qb, info);
   }
   return acc;
-}
-
-// the first VN trip's adjacency words (up to 4 per lane) of the layer [v0, v1)
-__device__ __forceinline__ void vn_preinfo(const uint32_t* adj_info, int v0, int v1, int lane, uint32_t (&pre)[4]) {
-#pragma unroll
-  for (int h = 0; h < 4; ++h) {
-    const int q = v0 + 64 * h + lane;
-    pre[h] = adj_info[q < v1 ? q : v0];
-  }
 }
 
 // Exact stop test (decoders.py:175-176): every row's parity of the current
@@ -1579,14 +1557,6 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
         const uint32_t dv = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uint32_t)adj_ptr[l] | ((uint32_t)adj_ptr[l + 1] << 16)));
         const int dsel = __builtin_amdgcn_readfirstlane((int)adj_dmax[l]);
         const int q0 = (int)(dq & 0xffffu), q1 = (int)(dq >> 16);
-        constexpr bool PRE = G == 1 && QLDPC_VN_PREINFO != 0;
-        uint32_t pre[4] = {0, 0, 0, 0};
-        if constexpr (PRE) {
-          // this layer's first VN adjacency words, in flight during the check
-          // nodes (the words never change); the one-lane-per-check instance only
-          const int pv0 = (int)(dv & 0xffffu), pv1 = (int)(dv >> 16);
-          if (pv0 < pv1) vn_preinfo(adj_info, pv0, pv1, lane, pre);
-        }
         if constexpr ((QLDPC_ABLATE_L & 1) != 0) {
         } else if constexpr (G != 0) {
           if constexpr (QLDPC_MSL_PRIO == 1) __builtin_amdgcn_s_setprio(1);
@@ -1614,8 +1584,8 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
           case -1: break;
 #define QLDPC_VN_CASE(K)                                                                \
   case K:                                                                               \
-    acc = v1 - v0 > 128 ? vn_layer<K, QLDPC_VN_H, PRE>(adj_info, avar, colS, c2v, v0, v1, lane, thr, pre) \
-                        : vn_layer<K, 2, PRE>(adj_info, avar, colS, c2v, v0, v1, lane, thr, pre);        \
+    acc = v1 - v0 > 128 ? vn_layer<K, QLDPC_VN_H>(adj_info, avar, colS, c2v, v0, v1, lane, thr) \
+                        : vn_layer<K, 2>(adj_info, avar, colS, c2v, v0, v1, lane, thr);        \
     break;
           QLDPC_VN_CASE(3) QLDPC_VN_CASE(4) QLDPC_VN_CASE(5) QLDPC_VN_CASE(6)
 #undef QLDPC_VN_CASE
@@ -1734,22 +1704,9 @@ __device__ __forceinline__ uint32_t cn_bp_word(const DecodeArgs& a, const qldpc_
   // lane-to-lane prefix chain, without its per-step index arithmetic, selects
   // and final broadcast (BP flooding is VALU-bound)
   const int base = lane & ~7;
-  double P;
-  if constexpr (QLDPC_BP_FOLD) {
-    // every permute issued before the first product: one LDS round trip of
-    // latency instead of DC - 1 in the fold's dependency chain
-    double tv[DC];
+  double P = __shfl(th, base, 64);
 #pragma unroll
-    for (int s = 0; s < DC; ++s) tv[s] = __shfl(th, base + s, 64);
-    __builtin_amdgcn_sched_barrier(0);
-    P = tv[0];
-#pragma unroll
-    for (int s = 1; s < DC; ++s) P = P * tv[s];
-  } else {
-    P = __shfl(th, base, 64);
-#pragma unroll
-    for (int s = 1; s < DC; ++s) P = P * __shfl(th, base + s, 64);
-  }
+  for (int s = 1; s < DC; ++s) P = P * __shfl(th, base + s, 64);
   // parity of the hard decisions of the posteriors this check read (:283-285)
   const uint64_t hb = ballot_b(ek && pj < 0.0);
   const uint32_t par = (uint32_t)__builtin_popcount((uint32_t)(hb >> (lane & 56)) & 0xffu) & 1u;
@@ -1877,7 +1834,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
           const int c = c0 + grp;
           const bool valid = c < m;
           const uint32_t sb = valid ? (synw[c >> 5] >> (c & 31)) & 1u : 0u;
-          unsat |= cn_bp_group<DC, QLDPC_BP_SAT_F>(a, g, valid ? c : 0, valid, k, lane, sb, post, c2v, fl);
+          unsat |= cn_bp_group<DC, false>(a, g, valid ? c : 0, valid, k, lane, sb, post, c2v, fl);
         }
         // the parity pass is the stop test of iteration it-1 (:283-285); its
         // team barrier also orders these c2v writes before the VN reads them
@@ -1890,10 +1847,8 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
         } else {
           __syncthreads();
         }
-        if constexpr (QLDPC_BP_FVNPRIO != 0) __builtin_amdgcn_s_setprio(QLDPC_BP_FVNPRIO);
         for (int j = tid; j < n; j += TS) post[j] = vn_post<ALGO_BP>(a, g, j, c2v, -1);
         __syncthreads();
-        if constexpr (QLDPC_BP_FVNPRIO != 0) __builtin_amdgcn_s_setprio(0);
         if (it + 1 == a.max_iter) {
           uint32_t un = 0;
           for (int c = tid; c < m; c += TS) {
@@ -1931,7 +1886,6 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
           }
           __syncthreads();
           // VN over the layer's adjacent variables
-          if constexpr (QLDPC_BP_FVNPRIO != 0) __builtin_amdgcn_s_setprio(QLDPC_BP_FVNPRIO);
           const int v0 = g.adj_ptr[l], v1 = g.adj_ptr[l + 1];
           uint32_t acc = 0;
           for (int q = v0 + tid; q < v1; q += TS) {
@@ -1944,7 +1898,6 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
           const uint32_t wacc = wave_xor(acc);
           if (lane == 0) fsl[wid] = wacc;
           __syncthreads();
-          if constexpr (QLDPC_BP_FVNPRIO != 0) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
           for (int w = 0; w < W; ++w) F ^= fsl[w];
           if (F == B) {                                   // team-uniform
@@ -2048,17 +2001,8 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
     for (int i = 0; i < NPF; ++i) {
       const int q = q0 + GP * i + grp;
       const bool v = q < q1;
-      if constexpr (QLDPC_BP_ULOAD) {
-        // every lane loads (a pad lane row 0, in bounds): no exec-masked
-        // loads, so the wait counts before the first use stay exact
-        const int qc = v ? q : 0;
-        const uint32_t w = ltab_g[8 * qc + k], r = lrow_g[qc];
-        pt[i] = (v && k < DC) ? w : 0u;
-        pc[i] = v ? r : 0u;
-      } else {
-        pt[i] = (v && k < DC) ? ltab_g[8 * q + k] : 0u;
-        pc[i] = v ? lrow_g[q] : 0u;
-      }
+      pt[i] = (v && k < DC) ? ltab_g[8 * q + k] : 0u;
+      pc[i] = v ? lrow_g[q] : 0u;
     }
   };
 
@@ -2098,12 +2042,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
 #pragma unroll
         for (int i = 0; i < NAF; ++i) {
           const int q = v0 + TS * i + tid;
-          if constexpr (QLDPC_BP_ULOAD) {
-            const uint32_t w = adj_g[q < v1 ? q : 0];     // unmasked load (slot 0 in bounds)
-            pa[i] = q < v1 ? w : 0u;
-          } else {
-            pa[i] = q < v1 ? adj_g[q] : 0u;
-          }
+          pa[i] = q < v1 ? adj_g[q] : 0u;
         }
 #pragma unroll
         for (int i = 0; i < NPF; ++i) {
@@ -2111,8 +2050,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
             const bool valid = q0 + GP * i + grp < q1;
             const int c = (int)pc[i];
             // (c = 0 for a pad check: an unmasked in-bounds read)
-            const uint32_t sb = (QLDPC_BP_ULOAD ? (synw[c >> 5] >> (c & 31)) & (valid ? 1u : 0u)
-                                                : (valid ? synw[c >> 5] >> (c & 31) : 0u)) & 1u;
+            const uint32_t sb = (valid ? synw[c >> 5] >> (c & 31) : 0u) & 1u;
             (void)cn_bp_word<DC, QLDPC_BP_SAT>(a, lt, pt[i], valid, k, lane, sb, post, c2v, fl);
           }
         }

@@ -236,3 +236,18 @@ extern "C" void qldpc_osd_keys_host(const double* h_post, int64_t count, double*
   else
     for (int64_t i = 0; i < count; ++i) h_key[i] = qldpc_osd_key(h_post[i]);
 }
+
+// The restated NumPy libm BP and the priors run (include/qldpc_libm.h, the
+// same code the kernels compile), element-wise on the host: the run-time pin
+// decoders.numpy_libm_pinned() compares it with the running NumPy.
+extern "C" int qldpc_libm_eval_host(int fn, const double* h_x, int64_t count, double* h_y) {
+  if (count < 0 || (count && (!h_x || !h_y))) return QLDPC_EINVAL;
+  switch (fn) {
+    case QLDPC_LIBM_TANH:  for (int64_t i = 0; i < count; ++i) h_y[i] = qldpc_tanh(h_x[i]); break;
+    case QLDPC_LIBM_ATANH: for (int64_t i = 0; i < count; ++i) h_y[i] = qldpc_atanh(h_x[i]); break;
+    case QLDPC_LIBM_LOG:   for (int64_t i = 0; i < count; ++i) h_y[i] = qldpc_np_log(h_x[i]); break;
+    case QLDPC_LIBM_EXP:   for (int64_t i = 0; i < count; ++i) h_y[i] = qldpc_np_exp(h_x[i]); break;
+    default: return QLDPC_EINVAL;
+  }
+  return QLDPC_OK;
+}

@@ -366,18 +366,16 @@ __device__ __forceinline__ int block_half(uint32_t (&lo)[SL], uint32_t (&hi)[SL]
   return K;
 }
 
-// block_half on the smallest power-of-two slot count >= SF (code per count),
-// or (QLDPC_OSD_SFEXACT) on exactly SF slots
+// block_half on the smallest power-of-two slot count >= SF (code per count)
 template <int SL, int SFMAX, bool HI>
 __device__ __forceinline__ int block_half_n(int SF, uint32_t (&lo)[SL], uint32_t (&hi)[SL], uint32_t (&cl)[SL],
                                             uint32_t (&ch)[SL], uint64_t (&fm)[SL], uint32_t cols, int K,
                                             int w, int lane, int& rank, int& nJ, bool& done, uint64_t& pivm,
                                             int rankH, int m, int& pkv) {
   if constexpr (SFMAX > 1) {
-    if (QLDPC_OSD_SFEXACT ? SF <= SFMAX - 1 : SF <= SFMAX / 2)
-      return block_half_n<SL, QLDPC_OSD_SFEXACT ? SFMAX - 1 : SFMAX / 2, HI>(SF, lo, hi, cl, ch, fm, cols, K, w,
-                                                                            lane, rank, nJ, done, pivm, rankH,
-                                                                            m, pkv);
+    if (SF <= SFMAX / 2)
+      return block_half_n<SL, SFMAX / 2, HI>(SF, lo, hi, cl, ch, fm, cols, K, w, lane, rank, nJ, done, pivm,
+                                             rankH, m, pkv);
   }
   return block_half<SL, SFMAX, HI>(lo, hi, cl, ch, fm, cols, K, w, lane, rank, nJ, done, pivm, rankH, m, pkv);
 }
@@ -564,7 +562,6 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
   }
   QLDPC_TICK(0);                                      // setup
   for (int w = 0; w < NW && 64 * w < n && !done; ++w) {   // done: uniform, re-read per block
-    if constexpr (QLDPC_OSD_APRIO != 0) __builtin_amdgcn_s_setprio(QLDPC_OSD_APRIO);
 #pragma unroll
     for (int h = 0; h < RT; ++h)                      // A
       if (own[h]) {
@@ -576,7 +573,6 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
       }
     __syncthreads();
     QLDPC_TICK(1);
-    if constexpr (QLDPC_OSD_APRIO != 0) __builtin_amdgcn_s_setprio(0);
     if (wave == engine) {                             // B
       // The engine is its shot's critical path while the SIMD also runs
       // other shots' phase-D waves: raised priority lets it issue first.

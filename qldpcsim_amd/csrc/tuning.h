@@ -12,14 +12,11 @@
     (defined(QLDPC_ABLATE) || defined(QLDPC_ABLATE_L) || defined(QLDPC_ABLATE_OSD) ||               \
      defined(QLDPC_OSD_TIMING) || defined(QLDPC_VN_PAIR) || defined(QLDPC_FLOOD_WPE) ||             \
      defined(QLDPC_VN_H) || defined(QLDPC_HBM_WAVES) || defined(QLDPC_HBM_UC) ||                    \
-     defined(QLDPC_OSD_WPE) || defined(QLDPC_OSD_PRIO) || defined(QLDPC_VN_PREINFO) ||                \
-     defined(QLDPC_ABLATE_ORD) || defined(QLDPC_OSD_DSPLIT) ||                                     \
-     defined(QLDPC_OSD_SFEXACT) || defined(QLDPC_MSL_GT) ||                                      \
-     defined(QLDPC_OSD_PAIRS) || defined(QLDPC_MSL_KARGS) || defined(QLDPC_BP_SAT) ||                \
-     defined(QLDPC_BP_FOLD) || defined(QLDPC_BP_SAT_F) || defined(QLDPC_BP_ULOAD) ||\
-     defined(QLDPC_BP_VNPRIO) || defined(QLDPC_BP_FVNPRIO) ||\
-     defined(QLDPC_BP_CNPRIO) || defined(QLDPC_BP_LHPRIO) ||\
-     defined(QLDPC_BP_FCNPRIO) || defined(QLDPC_MSL_PRIO) || defined(QLDPC_OSD_APRIO))
+     defined(QLDPC_OSD_WPE) || defined(QLDPC_OSD_PRIO) || defined(QLDPC_ABLATE_ORD) ||               \
+     defined(QLDPC_OSD_DSPLIT) || defined(QLDPC_MSL_GT) || defined(QLDPC_OSD_PAIRS) ||               \
+     defined(QLDPC_MSL_KARGS) || defined(QLDPC_BP_SAT) || defined(QLDPC_BP_VNPRIO) ||                \
+     defined(QLDPC_BP_CNPRIO) || defined(QLDPC_BP_LHPRIO) || defined(QLDPC_BP_FCNPRIO) ||            \
+     defined(QLDPC_MSL_PRIO))
 #error "kernel tuning knobs are for experiment builds: add -DQLDPC_EXPERIMENTS"
 #endif
 
@@ -63,19 +60,10 @@
 #define QLDPC_OSD_PRIO 3     // osd_block_kernel: s_setprio of the engine wave during phase B (0: none;
                              // 1 and 3 both -3.3 % per launch, profiles/r04am/)
 #endif
-#ifndef QLDPC_OSD_APRIO
-#define QLDPC_OSD_APRIO 0    // osd_block_kernel: phase A (the block's row words staged for the engine) at
-                             // this priority (0: none); 2: 22.37 -> 22.41 ms per 68,301 shots, not kept
-                             // (profiles/r05/osd_aprio_ab.jsonl)
-#endif
 #ifndef QLDPC_OSD_DSPLIT
 #define QLDPC_OSD_DSPLIT 12  // osd_block_kernel phase D: pivot-row words read in two batches when more
                              // than this many remain (0: one batch); 12: 93 -> 16 spilled VGPRs,
                              // 26.85 -> 26.56 ms per 68,301 shots (profiles/r05/osd_dsplit_ab.jsonl)
-#endif
-#ifndef QLDPC_OSD_SFEXACT
-#define QLDPC_OSD_SFEXACT 0  // osd_block_kernel phase B: code for every free-slot count 1..SL (1), or for
-                             // powers of two only (0)
 #endif
 #ifndef QLDPC_OSD_PAIRS
 #define QLDPC_OSD_PAIRS 1    // osd_block_kernel phase D: this block's pivots applied two at a time from
@@ -97,15 +85,6 @@
                              // tanh, the product, the division and the atanh (0: always the full path);
                              // LP118_2 p = 0.1 111.8 -> 107.6 ms per launch (profiles/r05/bp_sat_ab.json)
 #endif
-#ifndef QLDPC_BP_SAT_F
-#define QLDPC_BP_SAT_F 0     // the same in the flooding BP kernel (bp_team_kernel<false, ..>): its check
-                             // costs 2.9 % on the fixed-work LP118_0 decode, which never saturates
-#endif
-#ifndef QLDPC_BP_ULOAD
-#define QLDPC_BP_ULOAD 0     // bp_team_lg_kernel: row / adjacency prefetches and syndrome bits read by
-                             // every lane (pad lanes: slot 0) instead of under an exec mask (1: exact wait
-                             // counts, yet LP118_2 p = 0.1 107.5 -> 111.0 ms, profiles/r05/bp_uload_ab.json)
-#endif
 #ifndef QLDPC_BP_VNPRIO
 #define QLDPC_BP_VNPRIO 2    // bp_team_lg_kernel: s_setprio of a layer's variable-node phase (0: none);
                              // 2: LP118_2 p = 0.1 107.2 -> 103.8 ms per launch (the check-node phase at
@@ -121,7 +100,7 @@
 #define QLDPC_BP_FCNPRIO 2   // the same modes for the flooding BP kernel's check nodes; 2: LP118_0 BP-F
                              // fixed work 76.9 -> 73.4 ms per launch (profiles/r05/prio_msl_bpf_ab.json;
                              // 78.5 -> 76.7 on a slower box, round5_ab_start_vs_head.json); mode 1: +1.6 %,
-                             // with FVNPRIO 2: within noise (bpf_prio_modes_ab.json)
+                             // with the flooding VN at 2 as well: within noise (bpf_prio_modes_ab.json)
 #endif
 #ifndef QLDPC_MSL_PRIO
 #define QLDPC_MSL_PRIO 1     // ms_layered_kernel: check nodes at priority 1 (1) or variable nodes at 1 (2);
@@ -132,18 +111,11 @@
                              // 1: 102.1 -> 101.4 ms per LP118_2 p = 0.1 launch (bp_lhprio_ab.json); 2, or
                              // 3 with the VN at 3: within 0.1 % (bp_lhprio_levels_ab.json)
 #endif
-#ifndef QLDPC_BP_FVNPRIO
-#define QLDPC_BP_FVNPRIO 0   // the same for bp_team_kernel (flooding and the all-LDS layered fallback);
-                             // 2: LP118_0 BP-F fixed work 76.82 -> 76.73 ms (within noise), not kept
-#endif
-#ifndef QLDPC_BP_FOLD
-#define QLDPC_BP_FOLD 0      // BP check node: the group's t values all permuted before np.prod's fold (1:
-                             // +2.1 % per LP118_2 p = 0.1 launch, -0.8 % BP-F, profiles/r05/bp_fold_ab.json;
-                             // with the phase priorities +4.3 % / +0.9 %, bp_fold_prio_ab.json) or one
-                             // permute per fold step (0)
-#endif
-#ifndef QLDPC_VN_PREINFO
-#define QLDPC_VN_PREINFO 0     // ms_layered_kernel<DC, 1>: first VN adjacency words read at the layer head
-                               // (-0.85 % per LP118_2 p = 0.1 launch at 7 waves per CU, profiles/r04as/;
-                               // +1.5 % at 8 waves, profiles/r05/msl_vn_knobs_ab.json)
-#endif
+
+// Variants measured and not kept (their A/B records stay under profiles/r05/,
+// DESIGN.md §3): batched fold permutes (bp_fold_ab.json), unmasked BP
+// prefetches (bp_uload_ab.json), the saturated-check shortcut in flooding BP,
+// flooding-BP VN priority (bpf_prio_modes_ab.json), OSD phase-A priority
+// (osd_aprio_ab.jsonl), exact free-slot counts in the OSD engine, the layered
+// VN's layer-head adjacency reads (msl_vn_knobs_ab.json). Their code paths
+// were removed in round 6.

@@ -20,9 +20,12 @@ host and the device elimination again. `OSDdec` / `apply_osd` are the
 single-shot and host entry points (host C++ elimination).
 
 The restated order is NumPy 2.2.6's on x86-64 AVX512_SKX (the reference's
-capture host). At import, `numpy_order_pinned()` compares it with the running
+capture host). At first use, `numpy_order_pinned()` compares it with the running
 NumPy on a fixed set of tie-heavy rows; if they differ (another NumPy build
-or ISA dispatch), every OSD order is NumPy's own, computed on the host.
+or ISA dispatch), every OSD order is NumPy's own, computed on the host, and a
+RuntimeWarning says why. `numpy_libm_pinned()` does the same for the tanh /
+arctanh / log / exp restated for BP and the priors (BP is bit-exact only where
+it holds; checked at the first BP decode); `parity_pins()` reports both.
 
 Deviations from the reference (documented in DESIGN.md §7):
   * layers=None means flooding (the reference raises AttributeError on
@@ -45,7 +48,8 @@ from .schedule import pack_layers
 __all__ = ["MS_decoder", "BP_decoder", "OSDdec", "decode_batch", "DecodeResult", "osd_perm", "pack_bits",
            "unpack_bits",
            "osd_perms", "apply_osd", "apply_osd_device", "apply_osd_device_many", "osd_device_stage",
-           "osd_device_finish", "osd_host_orders", "osd_status_check"]
+           "osd_device_finish", "osd_host_orders", "osd_status_check", "numpy_order_pinned",
+           "numpy_libm_pinned", "parity_pins"]
 
 
 @dataclass
@@ -100,6 +104,8 @@ def decode_batch(H, syndromes, p, max_iter, layers=None, algo="MS", beta=0.75, e
     """
     if algo not in _lib.ALGO:
         raise ValueError("Unrecognized decoder type.")
+    if algo == "BP" and "libm" not in _PINNED:
+        numpy_libm_pinned()                   # once: warns if BP cannot be bit-exact on this NumPy
     H = np.asarray(H)
     m, n = H.shape
     if layer_ptr is None:
@@ -196,29 +202,95 @@ def _pin_rows():
     return rows
 
 
-_PINNED_ORDER = []
+_PINNED = {}                 # "order" / "libm" -> (bool, reason)
+
+
+def _pin_warn(what, reason):
+    import warnings
+    warnings.warn(f"qldpcsim_amd: {what} not pinned to the running NumPy {np.__version__} ({reason}); "
+                  + ("every OSD reliability order is computed by NumPy on the host (slower, same results)"
+                     if what == "reliability order" else
+                     "BP decodes follow the 1e-5 posterior contract instead of bit-exact parity"),
+                  RuntimeWarning, stacklevel=3)
 
 
 def numpy_order_pinned():
     """Whether the running NumPy's reliability order (np.exp, np.argsort)
     equals the restatement the device and the host library run
-    (qldpc_osd_order_host): checked once, on _pin_rows(), bit for bit."""
-    if not _PINNED_ORDER:
-        ok = True
+    (qldpc_osd_order_host): checked once, on _pin_rows(), bit for bit. When it
+    does not, a RuntimeWarning says why (missing library symbol, or the first
+    pin row whose order differs) and every OSD order is computed by NumPy on
+    the host; parity_pins() reports the reason."""
+    if "order" not in _PINNED:
+        ok, why = True, "equal on every pin row"
         try:
-            for P in _pin_rows():
+            for r, P in enumerate(_pin_rows()):
                 P = np.ascontiguousarray(P, np.float64)
                 n = P.size
                 perm = np.empty(n, np.int32)
                 st = np.empty(1, np.int32)
                 _lib.check(_lib.lib.qldpc_osd_order_host(_lib.ptr(P), 1, n, _lib.ptr(perm), _lib.ptr(st), 1))
                 if st[0] != 0 or not np.array_equal(perm, osd_perm(P)):
-                    ok = False
+                    ok, why = False, f"pin row {r} (n = {n}) orders differently"
                     break
-        except (OSError, AttributeError, RuntimeError):
-            ok = False
-        _PINNED_ORDER.append(ok)
-    return _PINNED_ORDER[0]
+        except (OSError, AttributeError, RuntimeError) as e:
+            ok, why = False, f"{type(e).__name__}: {e}"
+        _PINNED["order"] = (ok, why)
+        if not ok:
+            _pin_warn("reliability order", why)
+    return _PINNED["order"][0]
+
+
+def _libm_pin_args():
+    """Fixed arguments for numpy_libm_pinned, over the ranges BP and the
+    priors feed each function (decoders.py:147, :232, :254-259, :322)."""
+    rng = np.random.default_rng(20251226)
+    t = np.concatenate([rng.uniform(-40, 40, 6000), rng.uniform(-1, 1, 3000), rng.normal(0, 1e-4, 500),
+                        np.linspace(19.0, 20.0, 257), -np.linspace(19.0, 20.0, 257),
+                        [0.0, -0.0, 1e-300, -1e-300, 0.5, 24.0, 710.0, -710.0]])
+    a = np.concatenate([rng.uniform(-1, 1, 6000), 1 - rng.uniform(0, 1e-6, 500), -1 + rng.uniform(0, 1e-6, 500),
+                        [1 - 1e-9, -(1 - 1e-9), 0.0, -0.0, 1e-300, 0.5, -0.5]])
+    pr = rng.uniform(1e-5, 0.4, 3000)
+    lg = np.concatenate([(1 - pr) / pr, rng.uniform(1e-3, 1e3, 3000), np.exp(rng.uniform(-700, 700, 500))])
+    ex = np.concatenate([rng.uniform(-100, 100, 6000), rng.uniform(-706, 706, 1000), [0.0, -0.0, 100.0, -100.0]])
+    return {"tanh": (0, t, np.tanh), "atanh": (1, a, np.arctanh), "log": (2, lg, np.log), "exp": (3, ex, np.exp)}
+
+
+def numpy_libm_pinned():
+    """Whether the running NumPy's tanh / arctanh / log / exp equal the
+    restatement BP's kernels and the priors run (include/qldpc_libm.h, through
+    qldpc_libm_eval_host): checked once, bit for bit, on _libm_pin_args(). BP is
+    bit-exact against the reference only where this holds (DESIGN.md §4);
+    otherwise a RuntimeWarning says which function differs and parity_pins()
+    reports it."""
+    if "libm" not in _PINNED:
+        ok, why = True, "equal on every pin argument"
+        try:
+            for name, (fn, x, ref) in _libm_pin_args().items():
+                x = np.ascontiguousarray(x, np.float64)
+                y = np.empty_like(x)
+                _lib.check(_lib.lib.qldpc_libm_eval_host(fn, _lib.ptr(x), x.size, _lib.ptr(y)))
+                with np.errstate(all="ignore"):
+                    want = ref(x)
+                bad = np.flatnonzero(y.view(np.uint64) != want.view(np.uint64))
+                if bad.size:
+                    ok, why = False, f"np.{ref.__name__} differs on {bad.size} of {x.size} arguments (x = {x[bad[0]]!r})"
+                    break
+        except (OSError, AttributeError, RuntimeError) as e:
+            ok, why = False, f"{type(e).__name__}: {e}"
+        _PINNED["libm"] = (ok, why)
+        if not ok:
+            _pin_warn("the restated libm", why)
+    return _PINNED["libm"][0]
+
+
+def parity_pins():
+    """{"order": bool, "libm": bool, "numpy": version, "reasons": {...}}: the
+    run-time pins parity depends on (smoke() and bench.py report them)."""
+    numpy_order_pinned()
+    numpy_libm_pinned()
+    return {"order": _PINNED["order"][0], "libm": _PINNED["libm"][0], "numpy": np.__version__,
+            "reasons": {k: v[1] for k, v in _PINNED.items()}}
 
 
 def osd_perms(post, nthreads=None):

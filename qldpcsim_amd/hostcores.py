@@ -31,22 +31,23 @@ def process_cores():
     return n, " capped by ".join(how)
 
 
-def _pinned():
-    """Whether this process is pinned to a strict subset of the machine's CPUs
-    (a launcher that gives each rank its own CPU set)."""
-    try:
-        return len(os.sched_getaffinity(0)) < (os.cpu_count() or 1)
-    except AttributeError:
-        return False
+def _own_cpuset():
+    """Whether this rank's CPU set is known to be its own (not shared with the
+    node's other ranks): only when the launcher says so, QLDPC_RANK_CPUSET=own
+    (e.g. one `taskset` / numactl CPU list per rank). An affinity mask smaller
+    than the machine proves nothing: a container cpuset, a Slurm allocation or
+    a `taskset` around the launcher gives every rank the same mask."""
+    return os.environ.get("QLDPC_RANK_CPUSET", "").strip().lower() == "own"
 
 
 def rank_cores(cap=16):
-    """Host threads one rank should use, at most `cap`, at least 1: a rank
-    pinned to its own CPU set uses that set (already its share); otherwise the
-    process budget is the node's, divided among its ranks (LOCAL_WORLD_SIZE;
-    ranks started without it share the machine with nobody we know of)."""
+    """Host threads one rank should use, at most `cap`, at least 1: the
+    process budget (process_cores) divided among the node's ranks
+    (LOCAL_WORLD_SIZE; ranks started without it share the machine with nobody
+    we know of), unless the launcher declared each rank's CPU set its own
+    (QLDPC_RANK_CPUSET=own), which is then already the rank's share."""
     cores, _ = process_cores()
-    if _pinned():
+    if _own_cpuset():
         return max(1, min(cap, cores))
     local = os.environ.get("LOCAL_WORLD_SIZE", "1")
     share = max(1, int(local)) if local.isdigit() else 1

@@ -444,13 +444,15 @@ def simulate(HxFile: str, HzFile: str, p, shots: int = 1000, decType: str = "MS"
              decIterations: int = 99, decSchedule: str = "F", OSDorder: int = -1,
              rngSeed: Optional[int] = None, *, batch_size: Optional[int] = None, verbose: bool = True,
              return_results: bool = False, sampler: Optional[str] = None,
-             resultsFile: Optional[str] = None):
+             resultsFile: Optional[str] = None, on_point=None):
     """p-sweep + results table (simulator.py:319-347). Returns None like the
     reference unless return_results=True.
 
     resultsFile (extension): a JSON file the sweep writes after every
     p-point; a rerun with the same arguments skips the points already there
-    (resumable long sweeps). Only rank 0 writes it."""
+    (resumable long sweeps). Only rank 0 writes it.
+    on_point (extension): called as on_point(pT, result, seconds) after each
+    p-point this call computed (bench.py times the sweep's points with it)."""
     Hx = load_matrix(HxFile)
     Hz = load_matrix(HzFile)
     assert max(p) <= 1. and min(p) >= 0.
@@ -466,10 +468,13 @@ def simulate(HxFile: str, HzFile: str, p, shots: int = 1000, decType: str = "MS"
         if float(pT) in done:
             results.append(done[float(pT)])
             continue
+        t0 = time.perf_counter()
         r = simulate_p(Hx, Hz, p=pT, shots=shots, rngSeed=rngSeed, decType=decType,
                        decIterations=decIterations, decSchedule=decSchedule,
                        OSDorder=OSDorder, batch_size=batch_size, verbose=verbose,
                        sampler=sampler)
+        if on_point is not None:
+            on_point(pT, r, time.perf_counter() - t0)
         results.append(r)
         done[float(pT)] = r
         if resultsFile and rank == 0:

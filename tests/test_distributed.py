@@ -81,22 +81,39 @@ def _bench_leg_worker(rank, world, port, out):
     import bench
     from qldpcsim_amd import decoders
     decoders.decode_batch = _oracle_decode_batch_osd
-    out[rank] = bench.sim_leg(3, 24, dist, warmup_shots=0, sampler="host")
+    out[rank] = {"strong": bench.sim_leg(3, 25, dist, warmup_shots=0, sampler="host"),
+                 "weak": bench.sim_leg(3, 12, dist, warmup_shots=0, sampler="host", per_rank=True),
+                 "sweep": bench.sim_sweep_leg(4, 6, dist, warmup_shots=0, sampler="host")}
     dist.destroy_process_group()
 
 
-def test_bench_simulate_leg_two_ranks_gloo():
-    """bench.py's end-to-end configs[3] leg under two gloo ranks (the decode
-    replaced by the CPU oracle + host OSD here): both ranks report the same
-    all-reduced counters over both shares, per-rank rates and host cores, and
-    the OSD shots' host-order share (all of them on this host path)."""
+def test_bench_simulate_legs_two_ranks_gloo():
+    """bench.py's end-to-end legs under two gloo ranks (the decode replaced by
+    the CPU oracle + host OSD here): configs[3] as a fixed total split over
+    the ranks (strong: 25 shots = 13 + 12) and per rank (weak: 2 x 12), and
+    configs[4]'s four-point p-sweep through simulate's own p loop. Both ranks
+    report the same all-reduced counters, per-rank rates and host cores, the
+    OSD shots' host-order share (all of them on this host path), and one curve
+    point per p with its own counters."""
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_bench_leg_worker, args=(2, _free_port(), out), nprocs=2, join=True)
-    a, b = out[0], out[1]
-    assert a["counters"] == b["counters"] and a["shots"] == b["shots"] == 48 and a["n_ranks"] == 2
+    a, b = out[0]["strong"], out[1]["strong"]
+    assert a["counters"] == b["counters"] and a["shots"] == b["shots"] == 25 and a["n_ranks"] == 2
+    assert a["scaling"] == "strong" and sorted(r["shots"] for r in a["per_rank"]) == [12, 13]
     c = a["counters"]
-    assert c["decSuccessExact"] + c["decSuccessDegen"] <= 48 and a["value"] > 0
+    assert c["decSuccessExact"] + c["decSuccessDegen"] <= 25 and a["value"] > 0
     assert len(a["per_rank"]) == 2 and all(r["host_cores"] >= 1 and r["shots_per_s"] > 0 for r in a["per_rank"])
     assert a["osd_shots"] == sum(r["osd_shots"] for r in a["per_rank"]) > 0
     assert a["host_order_share"] == 1.0
+    w = out[0]["weak"]
+    assert w["scaling"] == "weak" and w["shots"] == 24 and [r["shots"] for r in w["per_rank"]] == [12, 12]
+    assert w["counters"] == out[1]["weak"]["counters"]
+    s0, s1 = out[0]["sweep"], out[1]["sweep"]
+    assert s0["p"] == [0.01, 0.02, 0.05, 0.1] and s0["scaling"] == "strong" and s0["n_ranks"] == 2
+    assert [pt["p"] for pt in s0["curve"]] == s0["p"] and all(pt["shots"] == 6 for pt in s0["curve"])
+    assert [pt["counters"] for pt in s0["curve"]] == [pt["counters"] for pt in s1["curve"]]
+    assert all(pt["value"] > 0 and 0.0 <= pt["qBLER"] <= 1.0 for pt in s0["curve"])
+    assert s0["elapsed_s"] >= max(pt["elapsed_s"] for pt in s0["curve"])
+    # BP never gets OSD from simulate (simulator.py:281-282); iterations are per shot
+    assert all(pt["counters"]["Avg_number_of_iterations_X"] >= 1.0 for pt in s0["curve"])

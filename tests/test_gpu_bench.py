@@ -34,11 +34,19 @@ def test_bench_single_gpu_line():
     r = _bench("--steps", "2", "--warmup", "1", "--batch", "65536", "--cpu-seconds", "1", "--sim-shots", "65536")
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
-    sim = {x["decType"]: x for x in d["simulate"]}            # the configs[3] / configs[4] legs
-    assert set(sim) == {"MS", "BP"} and all(x["shots"] == 65536 and x["value"] > 0 for x in sim.values())
-    assert sim["MS"]["osd_shots"] > 0 and sim["MS"]["host_order_shots"] == 0   # NumPy's order on the device
-    assert sim["BP"]["osd_shots"] == 0                         # simulate never passes OSDorder to BP
-    assert 0.5 < sim["MS"]["qBLER"] < 1.0
+    sim = d["simulate"]                                        # the configs[3] / configs[4] legs
+    c3, c4 = sim["configs3"], sim["configs4"]
+    assert c3["shots"] == 65536 and c3["value"] > 0 and c3["scaling"] == "strong"
+    assert c3["weak_per_rank"]["scaling"] == "weak" and c3["weak_per_rank"]["value"] == c3["value"]
+    assert c3["osd_shots"] > 0 and c3["host_order_shots"] == 0   # NumPy's order on the device
+    assert 0.5 < c3["qBLER"] < 1.0
+    # configs[4]: the four-point curve through simulate's p loop; the qBLER
+    # rises with p, and BP never gets OSD from simulate (simulator.py:281-282)
+    assert [pt["p"] for pt in c4["curve"]] == [0.01, 0.02, 0.05, 0.1]
+    assert all(pt["shots"] == 65536 and pt["value"] > 0 for pt in c4["curve"])
+    q = [pt["qBLER"] for pt in c4["curve"]]
+    assert q == sorted(q) and q[-1] > 0.1
+    assert d["parity_pin"]["order"] and d["parity_pin"]["libm"]
     assert KEYS <= set(d) and d["n_gpus"] == 1 and d["value"] > 0
     rf = d["roofline"]
     assert rf["kernel"] == "ms_flood_kernel<8, 4>"
@@ -91,10 +99,14 @@ def test_bench_spawns_ranks_itself_over_gloo():
     d = _last_json(r.stdout)
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * 16384
     assert "cpu_baseline" not in d and d["value"] > 0
-    leg, = d["simulate"]                                      # configs[3], each rank its share, one all-reduce
-    assert leg["n_ranks"] == 2 and leg["shots"] == 2 * 32768 and len(leg["per_rank"]) == 2
+    leg = d["simulate"]["configs3"]                           # a fixed total, each rank its share
+    assert leg["n_ranks"] == 2 and leg["shots"] == 32768 and len(leg["per_rank"]) == 2
+    assert [r["shots"] for r in leg["per_rank"]] == [16384, 16384]
     c = leg["counters"]
     assert 0 < c["decSuccessExact"] + c["decSuccessDegen"] < leg["shots"] and leg["host_order_shots"] == 0
+    weak = leg["weak_per_rank"]                               # 32768 per rank
+    assert weak["shots"] == 2 * 32768 and weak["scaling"] == "weak"
+    assert "configs4" not in d["simulate"]
 
 
 def test_bench_refuses_more_ranks_than_gpus_over_rccl():

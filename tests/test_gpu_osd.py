@@ -401,10 +401,12 @@ def test_device_osd_pipeline_matches_reference_at_configs3(order, device_min, os
     """configs[3]'s setting from the reference itself (tests/golden/
     ms_LP118_2_osd50.npz: LP118_2 MS layered, 50 iterations, p = 0.1): the
     device decode reproduces the reference's iterations and posteriors, then
-    the full device OSD path — device reliability order with its tie
-    certification, the status-2 host fallback (NumPy's order), block
-    elimination — reproduces the reference's OSD-0 / OSD-1 estimates on every
-    non-converged shot (decoders.py:179-180, :299-370)."""
+    the full device OSD path reproduces the reference's OSD-0 / OSD-1
+    estimates on every non-converged shot (decoders.py:179-180, :299-370).
+    device_min = 1: NumPy's reliability order computed on the device
+    (osd_order_kernel), with no shot left to a host order; device_min = 4096
+    (more than a golden batch's OSD shots): every order computed by NumPy on
+    the host. Both then run the block elimination on the device."""
     import torch
     from conftest import golden_cases, half_matrix
     from qldpcsim_amd import decoders

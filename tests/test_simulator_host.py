@@ -241,17 +241,25 @@ def test_large_codes_use_the_host_sampler():
     assert not simulator._channel_ok(np.zeros((3, 4097)), np.zeros((3, 4097)))
 
 
-def test_rank_cores_pinned_vs_shared(monkeypatch):
-    """hostcores.rank_cores: a rank pinned to its own CPU set uses that set;
-    an unpinned rank divides the machine's budget among the node's ranks."""
+def test_rank_cores_shared_unless_declared_own(monkeypatch):
+    """hostcores.rank_cores divides the process budget among the node's ranks
+    (LOCAL_WORLD_SIZE) — also when the affinity mask is smaller than the
+    machine, since a container cpuset / Slurm allocation / `taskset` on the
+    launcher gives every rank the same mask (8 ranks on a 16-CPU cpuset: 2
+    threads each, not 16) — and keeps a rank's whole set only when the
+    launcher declares it the rank's own (QLDPC_RANK_CPUSET=own)."""
     import os
     from qldpcsim_amd import hostcores
     monkeypatch.delenv("OMP_NUM_THREADS", raising=False)
+    monkeypatch.delenv("QLDPC_RANK_CPUSET", raising=False)
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
     monkeypatch.setattr(os, "cpu_count", lambda: 128)
-    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(16)))         # pinned: 16 of 128
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(16)))         # a shared 16-CPU cpuset
     monkeypatch.setattr(hostcores, "process_cores", lambda: (16, "sched_getaffinity"))
+    assert hostcores.rank_cores() == 2
+    monkeypatch.setenv("QLDPC_RANK_CPUSET", "own")                                    # one CPU set per rank
     assert hostcores.rank_cores() == 16
+    monkeypatch.delenv("QLDPC_RANK_CPUSET")
     monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(128)))        # whole machine, shared
     monkeypatch.setattr(hostcores, "process_cores", lambda: (128, "sched_getaffinity"))
     assert hostcores.rank_cores() == 16 and hostcores.rank_cores(cap=64) == 16
