@@ -15,8 +15,10 @@
 // [B, ceil(m/64)] (bit-packed words) on a HIP device; H [m, n] and the
 // schedule (layer_ptr [L+1], layer_rows, int32 or int64) as CPU tensors.
 // The cache is keyed by a 128-bit hash of H's own bytes (dtype and shape
-// included) and a hit is confirmed against the stored bytes, so a call with a
-// cached H reads it twice and copies nothing; torch.ops.qldpc.release()
+// included) and a hit is confirmed against the stored image of H: its mod-2
+// bits (1 bit per entry) for integer / bool H, its bytes otherwise — so a
+// call with a cached H reads it twice and copies nothing, and a cached
+// integer H costs m n / 8 bytes of host memory; torch.ops.qldpc.release()
 // waits for calls in flight, synchronizes the devices and frees the cache.
 // Errors as decode_batch / the reference: ValueError for shapes / options
 // (and for CPU syndromes: there is no CPU path), IndexError for layer rows out
@@ -26,6 +28,7 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/library.h>
 
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -40,7 +43,8 @@
 namespace {
 
 struct CodeEntry {
-  std::vector<unsigned char> bytes;                          // H's own bytes (confirms a hash hit)
+  std::vector<uint64_t> bits;                                // H mod 2, bit-packed (integer / bool H)
+  std::vector<unsigned char> bytes;                          // H's own bytes (floating-point H)
   qldpc_code* code = nullptr;
   std::map<std::vector<int32_t>, qldpc_schedule*> scheds;   // key: layer_ptr ++ layer_rows
 };
@@ -76,6 +80,38 @@ uint64_t hash_bytes(const unsigned char* p, size_t len, uint64_t seed) {
   h *= P2;
   h ^= h >> 29;
   return h;
+}
+
+// H mod 2 (load_matrix's `mat % 2`, simulator.py:35) bit-packed, for an
+// integer / bool H: for two's-complement integers v mod 2 == v & 1
+template <typename T>
+void pack_mod2(const T* h, size_t len, std::vector<uint64_t>& out) {
+  out.assign((len + 63) / 64, 0ull);
+  for (size_t i = 0; i < len; ++i) out[i >> 6] |= (uint64_t)((uint64_t)h[i] & 1u) << (i & 63);
+}
+template <typename T>
+bool same_mod2(const T* h, size_t len, const std::vector<uint64_t>& bits) {
+  if (bits.size() != (len + 63) / 64) return false;
+  for (size_t w = 0; w < bits.size(); ++w) {
+    uint64_t v = 0;
+    const size_t e = std::min(len, 64 * w + 64);
+    for (size_t i = 64 * w; i < e; ++i) v |= (uint64_t)((uint64_t)h[i] & 1u) << (i & 63);
+    if (v != bits[w]) return false;
+  }
+  return true;
+}
+// f(pointer) on H's typed data for the integer / bool dtypes; false otherwise
+template <typename F>
+bool with_int_data(const at::Tensor& H, F&& f) {
+  switch (H.scalar_type()) {
+    case at::kByte: f(H.data_ptr<uint8_t>()); return true;
+    case at::kChar: f(H.data_ptr<int8_t>()); return true;
+    case at::kShort: f(H.data_ptr<int16_t>()); return true;
+    case at::kInt: f(H.data_ptr<int32_t>()); return true;
+    case at::kLong: f(H.data_ptr<int64_t>()); return true;
+    case at::kBool: f(reinterpret_cast<const uint8_t*>(H.data_ptr<bool>())); return true;
+    default: return false;
+  }
 }
 
 void check(int rc) {
@@ -131,11 +167,16 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> decode_hip(
     std::lock_guard<std::mutex> lk(g_mu);
     std::vector<CodeEntry>& cands = g_codes[key];
     CodeEntry* hit = nullptr;
-    for (CodeEntry& c : cands)
-      if (c.bytes.size() == hbytes && memcmp(c.bytes.data(), hp, hbytes) == 0) hit = &c;
+    const size_t len = (size_t)Hc.numel();
+    for (CodeEntry& c : cands) {
+      bool same = false;
+      if (!with_int_data(Hc, [&](auto* h) { same = same_mod2(h, len, c.bits); }))
+        same = c.bytes.size() == hbytes && memcmp(c.bytes.data(), hp, hbytes) == 0;
+      if (same) hit = &c;
+    }
     if (!hit) {                                               // new H (or a hash collision)
       CodeEntry ne;
-      ne.bytes.assign(hp, hp + hbytes);
+      if (!with_int_data(Hc, [&](auto* h) { pack_mod2(h, len, ne.bits); })) ne.bytes.assign(hp, hp + hbytes);
       const at::Tensor Hb = Hc.remainder(2).to(at::kByte).contiguous();     // load_matrix's (mat % 2)
       check(qldpc_code_create(Hb.data_ptr<uint8_t>(), (int)m, (int)n, &ne.code));
       cands.push_back(std::move(ne));

@@ -20,6 +20,7 @@
 #   osd            tools/osd_bench.py on the configs[3] p = 0.1 OSD shots
 #   osdab:LIBS     interleaved A/B of the device OSD (tools/osd_bench.py, configs[3] p = 0.1) over library builds
 #   simab:LIBS     configs[3] sweep (tools/bench_sim.py) per library build, two interleaved rounds
+#   stall:LIBS:CFG SQ wave-state counters (WAIT_ANY / WAIT_INST_ANY / ACTIVE_*) per build, one cfg preset
 #   ab:LIBS:CFGS   interleaved A/B (tools/ab_libs.py) of qldpcsim_amd/_build/var_<name>.so builds;
 #                  LIBS = comma-separated names (main = the in-tree build; name+opt=v+opt=v adds
 #                  library options), CFGS = cfg preset names
@@ -167,6 +168,11 @@ for k in d: print(k, sorted(d[k]), sh[k])" ;;
       L=$O/${TAG}_ab_${libs//,/_}.json
       timeout -k 10 900 python -u tools/ab_libs.py --rounds 3 "${C[@]}" "${A[@]}" > $L 2>&1 || fail $step $? $L
       cat $L ;;
+    stall:*)
+      # SQ wave-state counters of one decode kernel per library build (tools/stall_profile.sh)
+      IFS=: read -r _ libs cfg <<< "$step"
+      timeout -k 10 900 bash tools/stall_profile.sh ${TAG}_$cfg "${CFG[$cfg]}" ${libs//,/ } > $O/${TAG}_stall_$cfg.log 2>&1 || fail $step $? $O/${TAG}_stall_$cfg.log
+      tail -40 $O/${TAG}_stall_$cfg.log ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
