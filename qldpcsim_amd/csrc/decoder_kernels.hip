@@ -113,8 +113,39 @@ __device__ __forceinline__ double np_sum_lt8(const double* a, int n) {
   return 0.0 + res;
 }
 
+// The same when every active lane's n >= 3 (round 6): -0.0 + x0 == x0 for
+// every x0, so the sum starts at x0; prefix sums over all K terms, and n
+// picks one of the last K - 2 (a compare and a 64-bit select each) instead of
+// a compare and select per term — the same float64 additions on the first n
+// terms, the same bits
+template <int K>
+__device__ __forceinline__ double np_sum_lt8_lo3(const double* a, int n) {
+  double x[K];
+#pragma unroll
+  for (int t = 0; t < K; ++t) x[t] = a[t];
+  double pre = x[0];
+#pragma unroll
+  for (int t = 1; t < 3; ++t) pre += x[t];
+  double res = pre;                                        // n = 3
+#pragma unroll
+  for (int t = 3; t < K; ++t) {
+    pre += x[t];                                           // (terms past n: discarded below)
+    res = n > t ? pre : res;
+  }
+  return 0.0 + res;
+}
+
+// LO3: try the n >= 3 form first (the layered team kernel: -0.7 % per LP118_2
+// p = 0.1 launch; the flooding kernel's extra ballot cost +0.7 %, so it keeps
+// the plain form, profiles/r06/r06d_ab_msnew_main.json)
+template <bool LO3 = false>
 __device__ __forceinline__ double np_sum_col(const double* a, int n) {
   if (__builtin_expect(ballot_b(n >= 8) != 0, 0)) return np_pairwise_sum(a, n);
+  if (LO3 && ballot_b(n < 3) == 0) {
+    if (ballot_b(n > 3) == 0) return np_sum_lt8_lo3<3>(a, n);
+    if (ballot_b(n > 5) == 0) return np_sum_lt8_lo3<5>(a, n);
+    return np_sum_lt8_lo3<7>(a, n);
+  }
   if (ballot_b(n > 3) == 0) return np_sum_lt8<3>(a, n);
   if (ballot_b(n > 5) == 0) return np_sum_lt8<5>(a, n);
   return np_sum_lt8<7>(a, n);
@@ -1341,7 +1372,12 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
 // QLDPC_VN_H (4: LP118_2's 240 / 480 in one / two passes instead of two / four,
 // -6.5 % per launch), smaller ones 2 (a 4-wide pass over <= 128 variables
 // idles half its lanes: LP118_0 +4 %)
-template <int K, int H>
+// LO (round 6): every variable of the layer has degree >= LO (host flag, bit
+// 7 of the layer's degree byte): the sum is formed as prefix sums over all K
+// slots and the degree picks one of the last K - LO + 1 of them, instead of a
+// compare and select per slot — the same float32 operations on the first d
+// terms, so the same bits (s never is -0.0: it starts as 0 + x0)
+template <int K, int H, int LO = 1>
 __device__ __forceinline__ uint32_t vn_layer(const uint32_t* adj_info, const uint32_t* avar, float* colS,
                                              const float* c2v, int v0, int v1, int lane, float thr) {
   uint32_t acc = 0;
@@ -1371,8 +1407,20 @@ __device__ __forceinline__ uint32_t vn_layer(const uint32_t* adj_info, const uin
     for (int h = 0; h < H; ++h) {
       const int d = (int)((info[h] >> 16) & 31u);
       float s = 0.0f;                                       // sequential, ascending check (:172)
+      if constexpr (LO > 1) {
+        float pre = 0.0f + x[h][0];
 #pragma unroll
-      for (int t = 0; t < K; ++t) s += (t < d) ? x[h][t] : 0.0f;
+        for (int t = 1; t < LO; ++t) pre += x[h][t];
+        s = pre;                                            // d = LO
+#pragma unroll
+        for (int t = LO; t < K; ++t) {
+          pre += x[h][t];                                   // (slots past d: discarded below)
+          s = d > t ? pre : s;
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < K; ++t) s += (t < d) ? x[h][t] : 0.0f;
+      }
       // every lane stores: a pad lane (past v1) holds variable v0's word and
       // computes exactly the value v0's own lane stored (same reads — the
       // c2v entries do not change in the VN — same sum), so no exec mask is
@@ -1526,6 +1574,21 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
   const int m = a.m, n = a.n;
   const float thr = a.hd_thresh;
 
+  // Layer bounds in registers (round 6): lane l holds layer l's row range,
+  // adjacency range and degree byte, read at each layer head by v_readlane
+  // instead of an LDS round trip (-3.5 % per LP118_2 p = 0.1 launch,
+  // profiles/r06/r06c_msl_lreg_ab.json); schedules of more than 64 layers
+  // (serial ones) keep the LDS reads (a uniform branch the compiler hoists)
+  const bool lreg = a.n_layers <= 64;
+  uint32_t lq_r = 0, lv_r = 0;
+  int ld_r = 0;
+  {
+    if (lane < a.n_layers) {
+      lq_r = (uint32_t)lay_ptr[lane] | ((uint32_t)lay_ptr[lane + 1] << 16);
+      lv_r = (uint32_t)adj_ptr[lane] | ((uint32_t)adj_ptr[lane + 1] << 16);
+      ld_r = (int)adj_dmax[lane];
+    }
+  }
   for (HalfShotQueue Q(a, waves, wid); Q.hs < a.batch; Q.advance()) {
     const long long hs = Q.hs;
     Q.prefetch(threadIdx.x & 63);
@@ -1553,9 +1616,17 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
     bool first = true;
     for (int it = 0; it < a.max_iter && !conv; ++it) {
       for (int l = 0; l < a.n_layers; ++l) {
-        const uint32_t dq = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uint32_t)lay_ptr[l] | ((uint32_t)lay_ptr[l + 1] << 16)));
-        const uint32_t dv = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uint32_t)adj_ptr[l] | ((uint32_t)adj_ptr[l + 1] << 16)));
-        const int dsel = __builtin_amdgcn_readfirstlane((int)adj_dmax[l]);
+        uint32_t dq, dv;
+        int dsel;
+        if (lreg) {
+          dq = (uint32_t)__builtin_amdgcn_readlane((int)lq_r, l);
+          dv = (uint32_t)__builtin_amdgcn_readlane((int)lv_r, l);
+          dsel = __builtin_amdgcn_readlane(ld_r, l);
+        } else {
+          dq = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uint32_t)lay_ptr[l] | ((uint32_t)lay_ptr[l + 1] << 16)));
+          dv = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uint32_t)adj_ptr[l] | ((uint32_t)adj_ptr[l + 1] << 16)));
+          dsel = __builtin_amdgcn_readfirstlane((int)adj_dmax[l]);
+        }
         const int q0 = (int)(dq & 0xffffu), q1 = (int)(dq >> 16);
         if constexpr ((QLDPC_ABLATE_L & 1) != 0) {
         } else if constexpr (G != 0) {
@@ -1566,7 +1637,7 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
           if constexpr (QLDPC_MSL_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         } else {
           // lanes per check chosen per layer by the host (bits 5-6 of adj_dmax)
-          switch (dsel >> 5) {
+          switch ((dsel >> 5) & 3) {
             case 0: cn_layer<DC, 1>(a, ltab, lrow, synw, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl); break;
             case 1: cn_layer<DC, 2>(a, ltab, lrow, synw, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl); break;
             case 2: cn_layer<DC, 4>(a, ltab, lrow, synw, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl); break;
@@ -1579,13 +1650,18 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
         // other columns are unchanged, so this equals the full recompute)
         const int v0 = (int)(dv & 0xffffu), v1 = (int)(dv >> 16);
         const int dmax = dsel & 31;
+        const bool lo3 = (dsel & 0x80) != 0;                // every adjacent variable of degree >= 3
         uint32_t acc = 0;
         switch ((QLDPC_ABLATE_L & 2) ? -1 : dmax) {
           case -1: break;
-#define QLDPC_VN_CASE(K)                                                                \
-  case K:                                                                               \
-    acc = v1 - v0 > 128 ? vn_layer<K, QLDPC_VN_H>(adj_info, avar, colS, c2v, v0, v1, lane, thr) \
-                        : vn_layer<K, 2>(adj_info, avar, colS, c2v, v0, v1, lane, thr);        \
+#define QLDPC_VN_CASE(K)                                                                              \
+  case K:                                                                                             \
+    if (lo3)                                                                                          \
+      acc = v1 - v0 > 128 ? vn_layer<K, QLDPC_VN_H, 3>(adj_info, avar, colS, c2v, v0, v1, lane, thr)  \
+                          : vn_layer<K, 2, 3>(adj_info, avar, colS, c2v, v0, v1, lane, thr);          \
+    else                                                                                              \
+      acc = v1 - v0 > 128 ? vn_layer<K, QLDPC_VN_H>(adj_info, avar, colS, c2v, v0, v1, lane, thr)     \
+                          : vn_layer<K, 2>(adj_info, avar, colS, c2v, v0, v1, lane, thr);             \
     break;
           QLDPC_VN_CASE(3) QLDPC_VN_CASE(4) QLDPC_VN_CASE(5) QLDPC_VN_CASE(6)
 #undef QLDPC_VN_CASE
@@ -2072,7 +2148,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
         auto vn = [&](uint32_t info) {
           const int j = (int)(info >> 21), d = (int)((info >> 16) & 31u);
           const double old = post[j];
-          const double sc = np_sum_col(c2v + (info & 0xffffu), d);
+          const double sc = np_sum_col<true>(c2v + (info & 0xffffu), d);
           const double nw = d == 0 ? L : L + sc;            // (:276-278)
           post[j] = nw;
           if ((old < 0.0) != (nw < 0.0)) acc ^= a.avar[j];
