@@ -1278,6 +1278,47 @@ __device__ __forceinline__ void group_merge(double& lo, double& hi, uint32_t& sh
   lo = nlo;
 }
 
+// Two lanes per check, every lane live (row degree 8: four edges per lane):
+// the one-lane-per-check instance's layers of at most 32 rows (round 6).
+// Lanes past the layer's last check repeat the trip's first check — the same
+// reads, the same values stored — so nothing is masked (as cn_layer's UNI).
+__device__ __forceinline__ void cn_ms_pair_uni(const DecodeArgs& a, const uint32_t* trow, int sub, uint32_t synb,
+                                               bool first, uint32_t post_b, uint32_t c2v_b, int& fl) {
+  const uint4 w = *(const uint4*)(trow + 4 * sub);
+  const uint32_t t[4] = {w.x, w.y, w.z, w.w};
+  double v[4];
+  uint32_t hv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (first) {
+      v[i] = (double)a.L32;                                       // (:148-149)
+    } else {
+      const double pj = a.L + (double)*QLDPC_LDS(const float, post_b + (t[i] & 0xffffu));   // (:173)
+      const float cv = *QLDPC_LDS(const float, c2v_b + (t[i] >> 16));
+      v[i] = pj - (double)cv;                                     // (:177)
+    }
+    hv[i] = hi_word(v[i]);
+  }
+  double lo, hi;
+  min12_tree<4>(v, lo, hi);
+  uint32_t sh = xor_tree<4>(hv);                                  // (:157-159)
+  group_merge<kDppQuadXor1>(lo, hi, sh);
+  double m1 = lo, m2 = hi;
+  if (__builtin_expect(ballot((lo == 0.0) | (hi == __builtin_inf())) != 0, 0)) {
+    m1 = __builtin_isinf(lo) ? 0.0 : lo;                          // (:165)
+    m2 = __builtin_isinf(hi) ? 0.0 : hi;                          // (:166)
+    if (m1 == 0.0) fl |= FLAG_MIN_ZERO;
+  }
+  const uint32_t npm = ((sh >> 31) ^ synb) << 31;
+  const uint32_t c1n = __builtin_bit_cast(uint32_t, (float)(a.beta * m1)) ^ npm;
+  const uint32_t c2n = __builtin_bit_cast(uint32_t, (float)(a.beta * m2)) ^ npm;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t c = (__builtin_fabs(v[i]) == lo) ? c2n : c1n;   // (:167-168)
+    *QLDPC_LDS(uint32_t, c2v_b + (t[i] >> 16)) = c ^ (hv[i] & 0x80000000u);
+  }
+}
+
 template <int DC, int G>
 __device__ __forceinline__ void cn_ms_split(const DecodeArgs& a, const uint32_t* trow, int sub, bool live,
                                             uint32_t synb, bool first, uint32_t post_b, uint32_t c2v_b,
@@ -1632,7 +1673,21 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
         } else if constexpr (G != 0) {
           if constexpr (QLDPC_MSL_PRIO == 1) __builtin_amdgcn_s_setprio(1);
           if constexpr (QLDPC_MSL_PRIO == 2) __builtin_amdgcn_s_setprio(0);
-          cn_layer<DC, G, G == 1>(a, ltab, lrow, synw, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl);
+          if (G == 1 && DC == 8 && q1 - q0 <= 32) {
+            // a layer of at most 32 rows: two lanes per check (four edges
+            // each, one DPP merge) instead of half the wave repeating the
+            // first check: 33.40 -> 32.77 ms per LP118_2 p = 0.1 launch
+            // (profiles/r06/r06f_ab_g2s.json; the generic split check node
+            // instead: 34.25 ms)
+            for (int qb = q0; qb < q1; qb += 32) {
+              const int q = qb + (lane >> 1);
+              const int qs = q < q1 ? q : qb;
+              const int c = lrow[qs];
+              const uint32_t sb = (synw[c >> 5] >> (c & 31)) & 1u;
+              cn_ms_pair_uni(a, ltab + qs * 8, lane & 1, sb, first, post_b, c2v_a, fl);
+            }
+          } else
+            cn_layer<DC, G, G == 1>(a, ltab, lrow, synw, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl);
           if constexpr (QLDPC_MSL_PRIO == 1) __builtin_amdgcn_s_setprio(0);
           if constexpr (QLDPC_MSL_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         } else {
