@@ -530,17 +530,26 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
         for (int e = code->row_ptr[r], k = 0; e < code->row_ptr[r + 1]; ++e, ++k)
           ltab[8 * q + k] = ((uint32_t)(4 * code->edge_pos[e]) << 16) | (uint32_t)(4 * code->vinv[code->col_idx[e]]);
       }
-      std::vector<uint8_t> adj_dmax(std::max(n_layers, 1), 0);
+      std::vector<uint16_t> adj_dmax(std::max(n_layers, 1), 0);
       for (int l = 0; l < n_layers; ++l) {
         int dmin = 32;
+        bool mid = false;                                   // a degree strictly between 3 and dmax
         for (int q = adj_ptr[l]; q < adj_ptr[l + 1]; ++q) {
           const int v = adj_vars[q], d = code->csc_ptr[v + 1] - code->csc_ptr[v];
           adj_info[q] = ((uint32_t)v << 21) | ((uint32_t)d << 16) | (uint32_t)code->csc_ptr[v];
-          adj_dmax[l] = (uint8_t)std::max<int>(adj_dmax[l], d);   // d <= 31 here
+          adj_dmax[l] = (uint16_t)std::max<int>(adj_dmax[l], d);   // d <= 31 here
           dmin = std::min(dmin, d);
         }
-        // bit 7: every adjacent variable has degree >= 3 (vn_layer's LO = 3)
-        if (dmin >= 3 && adj_ptr[l + 1] > adj_ptr[l]) adj_dmax[l] = (uint8_t)(adj_dmax[l] | 0x80);
+        for (int q = adj_ptr[l]; q < adj_ptr[l + 1]; ++q) {
+          const int v = adj_vars[q], d = code->csc_ptr[v + 1] - code->csc_ptr[v];
+          mid |= d > 3 && d < adj_dmax[l];
+        }
+        // bit 7: every adjacent variable has degree >= 3 (vn_layer's LO = 3);
+        // bit 8: and every degree is 3 or the layer's maximum (vn_layer's TWO)
+        if (dmin >= 3 && adj_ptr[l + 1] > adj_ptr[l]) {
+          adj_dmax[l] = (uint16_t)(adj_dmax[l] | 0x80);
+          if (!mid) adj_dmax[l] = (uint16_t)(adj_dmax[l] | 0x100);
+        }
       }
       // bits 5-6: log2 of the layer's lanes per check (ms_layered_kernel<DC, 0>):
       // one lane per check for long layers, a lane group when the layer leaves
@@ -550,7 +559,7 @@ extern "C" int qldpc_schedule_create(const qldpc_code* code, int n_layers, const
       for (int l = 0; l < n_layers; ++l) {
         const int rows = lay_ptr[l + 1] - lay_ptr[l];
         const int gl = rows <= 8 ? 3 : (rows <= 16 ? 2 : 0);
-        adj_dmax[l] = (uint8_t)(adj_dmax[l] | (gl << 5));
+        adj_dmax[l] = (uint16_t)(adj_dmax[l] | (gl << 5));
         s->layer_g = (s->layer_g == -2 || s->layer_g == (1 << gl)) ? (1 << gl) : 0;
       }
       {

@@ -1418,7 +1418,10 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
 // slots and the degree picks one of the last K - LO + 1 of them, instead of a
 // compare and select per slot — the same float32 operations on the first d
 // terms, so the same bits (s never is -0.0: it starts as 0 + x0)
-template <int K, int H, int LO = 1>
+// TWO (round 6): every degree is LO or K (bit 8; LP118_2's 3 / 5): one select
+// of the two prefix sums (32.42 -> 31.71 ms per LP118_2 p = 0.1 launch,
+// profiles/r06/r06h_ab_msl_two_min.json)
+template <int K, int H, int LO = 1, bool TWO = false>
 __device__ __forceinline__ uint32_t vn_layer(const uint32_t* adj_info, const uint32_t* avar, float* colS,
                                              const float* c2v, int v0, int v1, int lane, float thr) {
   uint32_t acc = 0;
@@ -1456,14 +1459,15 @@ __device__ __forceinline__ uint32_t vn_layer(const uint32_t* adj_info, const uin
 #pragma unroll
         for (int t = LO; t < K; ++t) {
           pre += x[h][t];                                   // (slots past d: discarded below)
-          s = d > t ? pre : s;
+          if constexpr (!TWO) s = d > t ? pre : s;
         }
+        if constexpr (TWO) s = d > LO ? pre : s;            // every degree is LO or K
       } else {
 #pragma unroll
         for (int t = 0; t < K; ++t) s += (t < d) ? x[h][t] : 0.0f;
       }
-      // every lane stores: a pad lane (past v1) holds variable v0's word and
-      // computes exactly the value v0's own lane stored (same reads — the
+      // every lane stores: a pad lane (past v1) holds variable v1 - 1's word
+      // and computes exactly the value that variable's lane stored (same reads — the
       // c2v entries do not change in the VN — same sum), so no exec mask is
       // needed around the store (-4.1 % per LP118_2 p = 0.1 launch,
       // -4.9 % LP118_0, profiles/r04ax/)
@@ -1477,7 +1481,7 @@ __device__ __forceinline__ uint32_t vn_layer(const uint32_t* adj_info, const uin
 #pragma unroll
     for (int h = 0; h < H; ++h) {
       const int q = qb + 64 * h + lane;
-      info[h] = adj_info[q < v1 ? q : v0];
+      info[h] = adj_info[min(q, v1 - 1)];
     }
     trip(qb, info);
   }
@@ -1513,13 +1517,13 @@ __device__ __forceinline__ void cn_layer(const DecodeArgs& a, const uint32_t* lt
                                          uint32_t c2v_a, int& fl) {
   if constexpr (GG == 1) {
     // UNI (the one-lane-per-check kernel instance): a wave-uniform loop —
-    // lanes past the layer's last check repeat the trip's first check (the
+    // lanes past the layer's last check repeat that check (one v_min; the
     // same reads, all issued before any store, so they store exactly its
     // values) instead of sitting out under an exec mask: -0.9 % per LP118_2
     // p = 0.1 launch, but +2.1 % inside the per-layer switch of LP118_0's
     // instance, which keeps the masked loop (profiles/r04ay/)
     for (int qi = UNI ? q0 : q0 + lane; qi < q1; qi += 64) {
-      const int q = !UNI ? qi : (qi + lane < q1 ? qi + lane : qi);
+      const int q = !UNI ? qi : min(qi + lane, q1 - 1);
       uint32_t t[1][8];
       load_row8(ltab + q * 8, t[0]);
       const int c = lrow[q];
@@ -1596,7 +1600,7 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
   const uint16_t* lay_ptr = (const uint16_t*)(lds + a.off_lay_ptr - sk);  // [L+1]
   const uint16_t* adj_ptr = (const uint16_t*)(lds + a.off_adj_ptr - sk);  // [L+1]
   const uint32_t* adj_info = (const uint32_t*)(lds + a.off_row_ptr - sk); // [A] var<<21 | deg<<16 | csc start
-  const uint8_t* adj_dmax = (const uint8_t*)(lds + a.off_chunk_dmax - sk);// [L] max degree per layer
+  const uint16_t* adj_dmax = (const uint16_t*)(lds + a.off_chunk_dmax - sk);// [L] max degree per layer
   const uint32_t* avar = [&]() {                                         // [n] filter word per variable
     if constexpr (GT != 0) return a.avar;
     else return (const uint32_t*)(lds + a.off_vn_chk - sk);
@@ -1681,7 +1685,7 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
             // instead: 34.25 ms)
             for (int qb = q0; qb < q1; qb += 32) {
               const int q = qb + (lane >> 1);
-              const int qs = q < q1 ? q : qb;
+              const int qs = min(q, q1 - 1);
               const int c = lrow[qs];
               const uint32_t sb = (synw[c >> 5] >> (c & 31)) & 1u;
               cn_ms_pair_uni(a, ltab + qs * 8, lane & 1, sb, first, post_b, c2v_a, fl);
@@ -1706,12 +1710,16 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
         const int v0 = (int)(dv & 0xffffu), v1 = (int)(dv >> 16);
         const int dmax = dsel & 31;
         const bool lo3 = (dsel & 0x80) != 0;                // every adjacent variable of degree >= 3
+        const bool two = (dsel & 0x100) != 0;               // ... and of degree 3 or dmax
         uint32_t acc = 0;
         switch ((QLDPC_ABLATE_L & 2) ? -1 : dmax) {
           case -1: break;
 #define QLDPC_VN_CASE(K)                                                                              \
   case K:                                                                                             \
-    if (lo3)                                                                                          \
+    if (K >= 5 && two)                                                                                \
+      acc = v1 - v0 > 128 ? vn_layer<K, QLDPC_VN_H, 3, K >= 5>(adj_info, avar, colS, c2v, v0, v1, lane, thr) \
+                          : vn_layer<K, 2, 3, K >= 5>(adj_info, avar, colS, c2v, v0, v1, lane, thr);  \
+    else if (lo3)                                                                                     \
       acc = v1 - v0 > 128 ? vn_layer<K, QLDPC_VN_H, 3>(adj_info, avar, colS, c2v, v0, v1, lane, thr)  \
                           : vn_layer<K, 2, 3>(adj_info, avar, colS, c2v, v0, v1, lane, thr);          \
     else                                                                                              \
