@@ -1288,17 +1288,23 @@ __device__ __forceinline__ void cn_ms_pair_uni(const DecodeArgs& a, const uint32
   const uint32_t t[4] = {w.x, w.y, w.z, w.w};
   double v[4];
   uint32_t hv[4];
+  if (first) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if (first) {
-      v[i] = (double)a.L32;                                       // (:148-149)
-    } else {
-      const double pj = a.L + (double)*QLDPC_LDS(const float, post_b + (t[i] & 0xffffu));   // (:173)
-      const float cv = *QLDPC_LDS(const float, c2v_b + (t[i] >> 16));
-      v[i] = pj - (double)cv;                                     // (:177)
+    for (int i = 0; i < 4; ++i) v[i] = (double)a.L32;            // (:148-149)
+  } else {
+    // the eight reads in one block, one wait: with the branch inside the edge
+    // loop the compiler gave each edge its own block and LDS round trip
+    float pf[4], cf[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      pf[i] = *QLDPC_LDS(const float, post_b + (t[i] & 0xffffu));
+      cf[i] = *QLDPC_LDS(const float, c2v_b + (t[i] >> 16));
     }
-    hv[i] = hi_word(v[i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = (a.L + (double)pf[i]) - (double)cf[i];   // (:173, :177)
   }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) hv[i] = hi_word(v[i]);
   double lo, hi;
   min12_tree<4>(v, lo, hi);
   uint32_t sh = xor_tree<4>(hv);                                  // (:157-159)
@@ -1341,19 +1347,24 @@ __device__ __forceinline__ void cn_ms_split(const DecodeArgs& a, const uint32_t*
   for (int i = 0; i < EPL; ++i) ek[i] = live && (DC == 8 || EPL * sub + i < DC);
   double v[EPL];
   uint32_t hv[EPL];
+  if (first) {
 #pragma unroll
-  for (int i = 0; i < EPL; ++i) {
-    if (first) {
-      v[i] = (double)a.L32;                                       // (:148-149)
-    } else {
-      // post_j = L + (f64)S_j rebuilt from the float32 column sum (exact: the
-      // value the reference stores, decoders.py:173)
-      const double pj = a.L + (double)*QLDPC_LDS(const float, post_b + (t[i] & 0xffffu));
-      const float cv = *QLDPC_LDS(const float, c2v_b + (t[i] >> 16));
-      v[i] = pj - (double)cv;                                     // v2c = post - c2v (:177)
+    for (int i = 0; i < EPL; ++i) v[i] = (double)a.L32;          // (:148-149)
+  } else {
+    // all reads in one block, one wait (as cn_ms_pair_uni)
+    float pf[EPL], cf[EPL];
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) {
+      pf[i] = *QLDPC_LDS(const float, post_b + (t[i] & 0xffffu));
+      cf[i] = *QLDPC_LDS(const float, c2v_b + (t[i] >> 16));
     }
-    hv[i] = ek[i] ? hi_word(v[i]) : 0u;
+    // post_j = L + (f64)S_j rebuilt from the float32 column sum (exact: the
+    // value the reference stores, decoders.py:173); v2c = post - c2v (:177)
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) v[i] = (a.L + (double)pf[i]) - (double)cf[i];
   }
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) hv[i] = ek[i] ? hi_word(v[i]) : 0u;
   double av[EPL];
 #pragma unroll
   for (int i = 0; i < EPL; ++i) av[i] = ek[i] ? v[i] : __builtin_inf();
