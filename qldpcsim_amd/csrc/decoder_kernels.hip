@@ -1551,13 +1551,21 @@ __device__ __forceinline__ void cn_layer(const DecodeArgs& a, const uint32_t* lt
       } else {
         CnLoad<DC> Ld;
         uint32_t ca[8];
+        float pf[8];
 #pragma unroll
         for (int k = 0; k < DC; ++k) {
           ca[k] = c2v_a + (t[0][k] >> 16);
-          Ld.pj[k] = a.L + (double)*QLDPC_LDS(const float, post_b + (t[0][k] & 0xffffu));   // (:173)
+          pf[k] = *QLDPC_LDS(const float, post_b + (t[0][k] & 0xffffu));
           Ld.cv[k] = *QLDPC_LDS(const float, ca[k]);
         }
-        const uint32_t sw = synw[c >> 5];
+        // every read issued before any arithmetic (left alone, the scheduler
+        // split the 16 reads over three round trips)
+        uint32_t sw = synw[c >> 5];
+#pragma unroll
+        for (int k = 0; k < DC; ++k) asm volatile("" : "+v"(pf[k]), "+v"(Ld.cv[k]));
+        asm volatile("" : "+v"(sw));
+#pragma unroll
+        for (int k = 0; k < DC; ++k) Ld.pj[k] = a.L + (double)pf[k];   // (:173)
         (void)cn_ms_compute<DC>(a, Ld, ca, (sw >> (c & 31)) & 1u, 1u, fl);
       }
     }
@@ -1854,6 +1862,8 @@ __device__ __forceinline__ uint32_t cn_bp_word(const DecodeArgs& a, const qldpc_
   // lane-to-lane prefix chain, without its per-step index arithmetic, selects
   // and final broadcast (BP flooding is VALU-bound)
   const int base = lane & ~7;
+  // (the permutes issued together before the fold, each waited for in turn
+  // now: +1 % per BP-L launch through register spills, r06k_ab_cn_reads_bp_shfl.json)
   double P = __shfl(th, base, 64);
 #pragma unroll
   for (int s = 1; s < DC; ++s) P = P * __shfl(th, base + s, 64);
