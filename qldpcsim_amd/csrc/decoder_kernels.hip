@@ -42,7 +42,7 @@ namespace qldpc {
 // NumPy's tanh / SVML's atanh tables (include/qldpc_libm.h). BP kernels copy
 // this image into LDS (DecodeArgs::off_libm) once per workgroup: the lookups
 // are per lane (data-dependent intervals), 10-13 per edge and iteration.
-__constant__ qldpc_libm_tab qldpc_libm_dev = QLDPC_LIBM_TAB_INIT;
+static __constant__ qldpc_libm_tab qldpc_libm_dev = QLDPC_LIBM_TAB_INIT;   // one per translation unit
 
 __device__ __forceinline__ const qldpc_libm_tab* stage_libm(unsigned char* lds, int off) {
   const uint4* src = (const uint4*)&qldpc_libm_dev;
@@ -2292,6 +2292,10 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
 // ---------------------------------------------------------------------------
 // Host-side launch helpers (called from capi.cpp)
 // ---------------------------------------------------------------------------
+// The BP team kernels are instantiated in their own translation unit
+// (bp_team_kernels.hip, built without SLP vectorization); every other kernel
+// here.
+#ifndef QLDPC_TU_BP_TEAM
 template <int ALGO, bool LAYERED, int DC>
 static const void* kernel_ptr() {
   return (const void*)&decode_kernel<ALGO, LAYERED, DC>;
@@ -2310,23 +2314,6 @@ const void* select_ms_flood_kernel(int dc, int kc, const char** name) {
   if (dc == 8 && kc <= 4) QLDPC_NAMED((&ms_flood_kernel<8, 4>), "ms_flood_kernel<8, 4>");
   if (dc == 7 && kc <= 8) QLDPC_NAMED((&ms_flood_kernel<7, 8>), "ms_flood_kernel<7, 8>");
   if (dc == 8 && kc <= 8) QLDPC_NAMED((&ms_flood_kernel<8, 8>), "ms_flood_kernel<8, 8>");
-  return nullptr;
-}
-
-const void* select_bp_team_kernel(bool layered, int dc, int w, const char** name) {
-#define QLDPC_BPT(L, D, Wn) \
-  if (layered == L && dc == D && w == Wn) QLDPC_NAMED((&bp_team_kernel<L, D, Wn>), "bp_team_kernel<" #L ", " #D ", " #Wn ">");
-  QLDPC_BPT(false, 7, 4) QLDPC_BPT(false, 8, 4) QLDPC_BPT(true, 7, 4) QLDPC_BPT(true, 8, 4)
-  QLDPC_BPT(false, 7, 8) QLDPC_BPT(false, 8, 8) QLDPC_BPT(true, 7, 8) QLDPC_BPT(true, 8, 8)
-#undef QLDPC_BPT
-  return nullptr;
-}
-
-const void* select_bp_team_lg_kernel(int dc, int w, const char** name) {
-  if (dc == 7 && w == 4) QLDPC_NAMED((&bp_team_lg_kernel<7, 4>), "bp_team_lg_kernel<7, 4>");
-  if (dc == 8 && w == 4) QLDPC_NAMED((&bp_team_lg_kernel<8, 4>), "bp_team_lg_kernel<8, 4>");
-  if (dc == 7 && w == 8) QLDPC_NAMED((&bp_team_lg_kernel<7, 8>), "bp_team_lg_kernel<7, 8>");
-  if (dc == 8 && w == 8) QLDPC_NAMED((&bp_team_lg_kernel<8, 8>), "bp_team_lg_kernel<8, 8>");
   return nullptr;
 }
 
@@ -2368,5 +2355,28 @@ hipError_t launch_decode(const void* kernel, const DecodeArgs& args, int grid, i
 hipError_t configure_kernel(const void* kernel, int lds_bytes) {
   return hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
 }
+
+#else  // QLDPC_TU_BP_TEAM
+
+#define QLDPC_NAMED(ptr, str) do { if (name) *name = str; return (const void*)ptr; } while (0)
+
+const void* select_bp_team_kernel(bool layered, int dc, int w, const char** name) {
+#define QLDPC_BPT(L, D, Wn) \
+  if (layered == L && dc == D && w == Wn) QLDPC_NAMED((&bp_team_kernel<L, D, Wn>), "bp_team_kernel<" #L ", " #D ", " #Wn ">");
+  QLDPC_BPT(false, 7, 4) QLDPC_BPT(false, 8, 4) QLDPC_BPT(true, 7, 4) QLDPC_BPT(true, 8, 4)
+  QLDPC_BPT(false, 7, 8) QLDPC_BPT(false, 8, 8) QLDPC_BPT(true, 7, 8) QLDPC_BPT(true, 8, 8)
+#undef QLDPC_BPT
+  return nullptr;
+}
+
+const void* select_bp_team_lg_kernel(int dc, int w, const char** name) {
+  if (dc == 7 && w == 4) QLDPC_NAMED((&bp_team_lg_kernel<7, 4>), "bp_team_lg_kernel<7, 4>");
+  if (dc == 8 && w == 4) QLDPC_NAMED((&bp_team_lg_kernel<8, 4>), "bp_team_lg_kernel<8, 4>");
+  if (dc == 7 && w == 8) QLDPC_NAMED((&bp_team_lg_kernel<7, 8>), "bp_team_lg_kernel<7, 8>");
+  if (dc == 8 && w == 8) QLDPC_NAMED((&bp_team_lg_kernel<8, 8>), "bp_team_lg_kernel<8, 8>");
+  return nullptr;
+}
+
+#endif  // QLDPC_TU_BP_TEAM
 
 }  // namespace qldpc
