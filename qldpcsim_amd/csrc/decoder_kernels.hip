@@ -2292,10 +2292,11 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))
 // ---------------------------------------------------------------------------
 // Host-side launch helpers (called from capi.cpp)
 // ---------------------------------------------------------------------------
-// The BP team kernels are instantiated in their own translation unit
-// (bp_team_kernels.hip, built without SLP vectorization); every other kernel
-// here.
-#ifndef QLDPC_TU_BP_TEAM
+// The BP team kernels and the flooding min-sum kernel are instantiated in
+// translation units of their own (bp_team_kernels.hip, built without SLP
+// vectorization; ms_flood_kernels.hip, built with the max-ILP machine
+// scheduler); every other kernel here.
+#if !defined(QLDPC_TU_BP_TEAM) && !defined(QLDPC_TU_FLOOD)
 template <int ALGO, bool LAYERED, int DC>
 static const void* kernel_ptr() {
   return (const void*)&decode_kernel<ALGO, LAYERED, DC>;
@@ -2305,17 +2306,6 @@ int ms_flood_max_waves(int kc) { return (kc >= 8 ? 512 : 256) / 64; }
 
 // Kernel names as rocprofv3 reports them (bench.py matches profiles by name).
 #define QLDPC_NAMED(ptr, str) do { if (name) *name = str; return (const void*)ptr; } while (0)
-
-const void* select_ms_flood_kernel(int dc, int kc, const char** name) {
-  // instantiated (DC, KC) shapes; the host passes ceil(m/64) checks per lane
-  if (dc == 7 && kc <= 2) QLDPC_NAMED((&ms_flood_kernel<7, 2>), "ms_flood_kernel<7, 2>");
-  if (dc == 8 && kc <= 2) QLDPC_NAMED((&ms_flood_kernel<8, 2>), "ms_flood_kernel<8, 2>");
-  if (dc == 7 && kc <= 4) QLDPC_NAMED((&ms_flood_kernel<7, 4>), "ms_flood_kernel<7, 4>");
-  if (dc == 8 && kc <= 4) QLDPC_NAMED((&ms_flood_kernel<8, 4>), "ms_flood_kernel<8, 4>");
-  if (dc == 7 && kc <= 8) QLDPC_NAMED((&ms_flood_kernel<7, 8>), "ms_flood_kernel<7, 8>");
-  if (dc == 8 && kc <= 8) QLDPC_NAMED((&ms_flood_kernel<8, 8>), "ms_flood_kernel<8, 8>");
-  return nullptr;
-}
 
 const void* select_ms_layered_kernel(int dc, int g, const char** name) {
 #define QLDPC_MSL(D, Gn) if (dc == D && g == Gn) QLDPC_NAMED((&ms_layered_kernel<D, Gn>), "ms_layered_kernel<" #D ", " #Gn ">");
@@ -2356,6 +2346,21 @@ hipError_t configure_kernel(const void* kernel, int lds_bytes) {
   return hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
 }
 
+#elif defined(QLDPC_TU_FLOOD)
+
+#define QLDPC_NAMED(ptr, str) do { if (name) *name = str; return (const void*)ptr; } while (0)
+
+const void* select_ms_flood_kernel(int dc, int kc, const char** name) {
+  // instantiated (DC, KC) shapes; the host passes ceil(m/64) checks per lane
+  if (dc == 7 && kc <= 2) QLDPC_NAMED((&ms_flood_kernel<7, 2>), "ms_flood_kernel<7, 2>");
+  if (dc == 8 && kc <= 2) QLDPC_NAMED((&ms_flood_kernel<8, 2>), "ms_flood_kernel<8, 2>");
+  if (dc == 7 && kc <= 4) QLDPC_NAMED((&ms_flood_kernel<7, 4>), "ms_flood_kernel<7, 4>");
+  if (dc == 8 && kc <= 4) QLDPC_NAMED((&ms_flood_kernel<8, 4>), "ms_flood_kernel<8, 4>");
+  if (dc == 7 && kc <= 8) QLDPC_NAMED((&ms_flood_kernel<7, 8>), "ms_flood_kernel<7, 8>");
+  if (dc == 8 && kc <= 8) QLDPC_NAMED((&ms_flood_kernel<8, 8>), "ms_flood_kernel<8, 8>");
+  return nullptr;
+}
+
 #else  // QLDPC_TU_BP_TEAM
 
 #define QLDPC_NAMED(ptr, str) do { if (name) *name = str; return (const void*)ptr; } while (0)
@@ -2377,6 +2382,6 @@ const void* select_bp_team_lg_kernel(int dc, int w, const char** name) {
   return nullptr;
 }
 
-#endif  // QLDPC_TU_BP_TEAM
+#endif  // translation units
 
 }  // namespace qldpc
