@@ -581,10 +581,18 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
       // crow[c] = the c-th free row; earlier pivots are reduced in phase D
       const int rank0 = rank;
       int F = 0;
+      // every read of a slot loop issued before the first use (left alone,
+      // each slot's read sat in its own exec-masked block with its own wait:
+      // 8 dependent LDS round trips on the engine's chain, twice per block)
+      int pv[SL];
+#pragma unroll
+      for (int s = 0; s < SL; ++s) pv[s] = pidx[64 * s + lane];     // (64 SL = MR row slots)
+#pragma unroll
+      for (int s = 0; s < SL; ++s) asm volatile("" : "+v"(pv[s]));
 #pragma unroll
       for (int s = 0; s < SL; ++s) {
         const int row = 64 * s + lane;
-        const bool fr = row < m && pidx[row] == m;
+        const bool fr = row < m && pv[s] == m;
         const uint64_t bf = __ballot(fr);
         if (fr) crow[F + __builtin_amdgcn_mbcnt_hi((uint32_t)(bf >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bf, 0))] = row;
         F += __builtin_popcountll(bf);
@@ -592,10 +600,20 @@ __global__ void __launch_bounds__(64 * SL / RT) __attribute__((amdgpu_waves_per_
       uint32_t lo[SL], hi[SL], cl[SL], ch[SL];
       uint64_t fm[SL];                                // slot s: lanes whose compact row is not yet a pivot
       uint32_t alo = 0, ahi = 0;                      // columns some free row holds
+      int cr[SL];
+#pragma unroll
+      for (int s = 0; s < SL; ++s) cr[s] = crow[64 * s + lane];     // (this wave's writes above: in order)
+#pragma unroll
+      for (int s = 0; s < SL; ++s) asm volatile("" : "+v"(cr[s]));
+      uint64_t wv[SL];
+#pragma unroll
+      for (int s = 0; s < SL; ++s) wv[s] = Wd[64 * s + lane < F ? cr[s] : 0];
+#pragma unroll
+      for (int s = 0; s < SL; ++s) asm volatile("" : "+v"(wv[s]));
 #pragma unroll
       for (int s = 0; s < SL; ++s) {
         const int cp = 64 * s + lane;
-        const uint64_t v = cp < F ? Wd[crow[cp]] : 0ull;
+        const uint64_t v = cp < F ? wv[s] : 0ull;
         lo[s] = (uint32_t)v;
         hi[s] = (uint32_t)(v >> 32);
         cl[s] = ch[s] = 0;
