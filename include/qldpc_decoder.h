@@ -170,7 +170,10 @@ int qldpc_osd_decode_batch(const qldpc_code *code, int64_t count, const uint8_t 
  * Same semantics as qldpc_osd_decode (orders 0, 1, >= 2) for `count` shots:
  * d_syn uint8[count][m], d_perm int32[count][n] (NumPy's reliability order),
  * d_ehat uint8[count][n] in/out, d_status int32[count] (0 ok; 1 = the
- * reference's IndexError case, e_hat left unchanged). m <= 1024, n <= 2111. */
+ * reference's IndexError case, e_hat left unchanged). Any size: m <= 1024 and
+ * n <= 2111 run in registers / LDS, larger codes with each shot's working
+ * matrix in device memory (osd_hbm_kernel; LDS holds one 64-bit word per row,
+ * so m is bounded by the LDS size, about 19,000 rows: QLDPC_EUNSUP past it). */
 int qldpc_osd_device(const qldpc_code *code, int64_t count, const uint8_t *d_syn,
                      const int32_t *d_perm, int order, uint8_t *d_ehat, int32_t *d_status,
                      void *stream);
@@ -312,6 +315,7 @@ int qldpc_timing_read(double *total_ms, int64_t *launches);
  *   "osd_column" (0)          GPU OSD through the exact-REF column kernel only
  *   "osd_tickets" (1)         GPU OSD engine wave placed by per-CU SIMD tickets
  *   "osd_prof" (0)            print per-phase OSD cycles (builds with QLDPC_OSD_TIMING)
+ *   "osd_hbm" (0)             GPU OSD through the device-memory kernel at any size (tests)
  * Unknown name: QLDPC_EINVAL. */
 int qldpc_set_option(const char *name, int64_t value);
 int qldpc_get_option(const char *name, int64_t *value);

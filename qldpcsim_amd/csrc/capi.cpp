@@ -73,7 +73,7 @@ namespace {
 struct Options {
   std::atomic<int64_t> force_hbm{0}, flood_generic{0}, layered_generic{0}, ms_lanes_per_check{0}, bp_wave{0},
       bp_lg{1}, bp_team_w{0}, static_sched{0}, waves_per_wg{0}, wg_per_cu{0}, osd_column{0}, osd_tickets{1},
-      osd_prof{0};
+      osd_prof{0}, osd_hbm{0};
   std::atomic<uint32_t> gen{1};
 };
 Options g_opt;
@@ -90,7 +90,7 @@ std::atomic<int64_t>* option_slot(const char* name) {
                {"bp_team_w", &Options::bp_team_w},     {"static_sched", &Options::static_sched},
                {"waves_per_wg", &Options::waves_per_wg}, {"wg_per_cu", &Options::wg_per_cu},
                {"osd_column", &Options::osd_column},   {"osd_tickets", &Options::osd_tickets},
-               {"osd_prof", &Options::osd_prof}};
+               {"osd_prof", &Options::osd_prof},       {"osd_hbm", &Options::osd_hbm}};
   for (const auto& e : table)
     if (strcmp(e.name, name) == 0) return &(g_opt.*(e.slot));
   return nullptr;
@@ -1624,6 +1624,79 @@ extern "C" int qldpc_osd_device_ordered_ex(const qldpc_code* code, int64_t count
   return rc;
 }
 
+// osd_hbm_kernel: one workgroup per shot, the shot's working matrix in a
+// per-shot slice of a stream-ordered scratch allocation (chunks of at most
+// 1 GiB of slices), LDS = one 64-bit word per row + small
+static int osd_hbm_impl(const qldpc_code* code, int64_t count, const uint8_t* d_syn, const int32_t* d_perm,
+                        const int32_t* d_tiepos, const double* d_post, int order, uint8_t* d_ehat,
+                        int32_t* d_status, void* stream) {
+  const int m = code->m, n = code->n;
+  const int nwr = (n + 1 + 63) / 64, mp = (m + 63) / 64 * 64;
+  int dev = 0, max_lds = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  HIP_TRY(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
+  const size_t lds = qldpc::osd_hbm_lds(m, nwr);
+  if (lds > (size_t)max_lds)
+    return fail(QLDPC_EUNSUP, "GPU OSD keeps one word per row in LDS: m = %d needs %zu B (at most %d)", m, lds,
+                max_lds);
+  const void* k = qldpc::osd_hbm_kernel_ptr();
+  HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  code_osd_prep(code);
+  auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  qldpc::OsdHbmArgs h{};
+  size_t off = up((size_t)8 * nwr * mp);
+  h.off_inv = (int)off;
+  off = up(off + 4 * (size_t)n);
+  h.off_jl = (int)off;
+  off = up(off + 4 * ((size_t)m + 2));
+  h.off_inj = (int)off;
+  off = up(off + (size_t)n);
+  h.off_table = (int)off;
+  if (order == 1) off = up(off + 4 * (size_t)setdiff_table_ints(n));
+  if (off > (size_t)INT32_MAX) return fail(QLDPC_EUNSUP, "GPU OSD scratch per shot exceeds 2 GiB (m = %d, n = %d)", m, n);
+  h.stride = (long long)off;
+  h.nwr = nwr;
+  h.mp = mp;
+  const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(count, 1 << 30),
+                                                                   ((int64_t)1 << 30) / (int64_t)off));
+  void* scr = nullptr;
+  HIP_TRY(hipMallocAsync(&scr, (size_t)chunk * off, (hipStream_t)stream));
+  h.scratch = (unsigned char*)scr;
+  qldpc::OsdArgs a{};
+  a.row_ptr = code->d_row_ptr;
+  a.col_idx = code->d_col_idx;
+  a.m = m;
+  a.n = n;
+  a.rank = code->rank;
+  a.order = order;
+  a.post = d_tiepos ? d_post : nullptr;
+  if (d_tiepos && g_spill.count) {
+    a.spill_post = g_spill.post;
+    a.spill_idx = g_spill.idx;
+    a.spill_count = g_spill.count;
+    a.spill_cap = g_spill.cap;
+  }
+  const int block = std::min(1024, std::max(64, mp));
+  hipError_t e = hipSuccess;
+  for (int64_t done = 0; done < count && e == hipSuccess; done += chunk) {
+    const int64_t g = std::min<int64_t>(count - done, chunk);
+    qldpc::OsdArgs ai = a;
+    ai.perm = d_perm + done * n;
+    ai.syn = d_syn + done * m;
+    ai.ehat = d_ehat + done * n;
+    ai.status = d_status + done;
+    ai.tiepos = d_tiepos ? d_tiepos + done : nullptr;
+    if (ai.post) ai.post = d_post + done * n;
+    ai.shot_base = done;
+    void* params[] = {(void*)&ai, (void*)&h};
+    e = hipLaunchKernel(k, dim3((unsigned)g), dim3(block), params, lds, (hipStream_t)stream);
+  }
+  const hipError_t ef = hipFreeAsync(scr, (hipStream_t)stream);
+  HIP_TRY(e);
+  HIP_TRY(ef);
+  return QLDPC_OK;
+}
+
 static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t* d_syn, const int32_t* d_perm,
                            const int32_t* d_tiepos, const double* d_post, int order, uint8_t* d_ehat,
                            int32_t* d_status, void* stream) {
@@ -1633,10 +1706,12 @@ static int osd_device_impl(const qldpc_code* code, int64_t count, const uint8_t*
   if (code->device < 0) return fail(QLDPC_EHIP, "no HIP device was visible when the code was created");
   if (!d_syn || !d_perm || !d_ehat || !d_status) return fail(QLDPC_EINVAL, "null device buffer");
   const int m = code->m, n = code->n;
-  if (m > 1024) return fail(QLDPC_EUNSUP, "GPU OSD supports m <= 1024 rows (got %d)", m);
   const int nw = qldpc::osd_nw_of((n + 1 + 63) / 64);
   const void* kcol = qldpc::select_osd_kernel(nw);
-  if (!kcol) return fail(QLDPC_EUNSUP, "GPU OSD supports n <= 2111 columns (got %d)", n);
+  // past the register / LDS kernels (m > 1024 rows, n > 2111 columns), or
+  // option osd_hbm: the working matrix in global memory (osd_hbm_kernel)
+  if (m > 1024 || !kcol || opt(&Options::osd_hbm) != 0)
+    return osd_hbm_impl(code, count, d_syn, d_perm, d_tiepos, d_post, order, d_ehat, d_status, stream);
   // The block kernel picks pivot rows by row index instead of REF's row
   // order: same J, same e_J (the unique solution), except when column 0 of
   // H[:, perm] has no pivot (an all-zero column of H: column kernel for the

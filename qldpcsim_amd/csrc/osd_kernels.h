@@ -43,6 +43,21 @@ constexpr int kOsdCuSlots = 16 * 256;  // XCC id (4 bits) x HW_ID bits 8-15 (CU,
 hipError_t launch_osd_order(const OrderArgs& a, long long count, hipStream_t stream);
 size_t osd_order_lds(int n);
 
+// osd_hbm_kernel (any m, n): each shot's working matrix lives in a global
+// scratch slice instead of VGPRs / LDS. Per shot, at `scratch + shot *
+// stride` (shot = the launch's blockIdx.x): R [nwr][mp] u64 (word-major: word
+// q of the row at REF position p at q * mp + p; nwr = ceil((n + 1) / 64), mp =
+// m rounded up to 64), then inv_perm [n] i32 at off_inv, the J list [m + 2]
+// i32 at off_jl, inJ [n] bytes at off_inj and the CPython set table (order 1)
+// at off_table. LDS: the current word of every row [mp] u64 + 3 [nwr] u64 + 160 B.
+struct OsdHbmArgs {
+  unsigned char* scratch;
+  long long stride;
+  int nwr, mp, off_inv, off_jl, off_inj, off_table;
+};
+const void* osd_hbm_kernel_ptr();        // __global__ osd_hbm_kernel(OsdArgs, OsdHbmArgs)
+inline size_t osd_hbm_lds(int m, int nwr) { return 8 * (size_t)((m + 63) / 64 * 64) + 24 * (size_t)nwr + 160; }
+
 const void* select_osd_kernel(int nw);  // nw = 64-bit words per row incl. the syndrome column
 const void* select_osd_block_kernel(int nw, int m, int* rows_per_thread);  // block elimination (default), same arguments
 int osd_nw_of(int nw);

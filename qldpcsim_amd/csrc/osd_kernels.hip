@@ -224,6 +224,8 @@ __global__ void __launch_bounds__(1024) osd_kernel(OsdArgs a) {
     }
     ehat[perm[Jl[t]]] = (uint8_t)(acc & 1ull);                // e_hat[perm] = ... (:368)
   }
+  if (t == 0)                                                  // (J past T sJ's m rows: 0, as
+    for (int p = m; p < nJ; ++p) ehat[perm[Jl[p]]] = 0;        // the host OSD; osd_hbm_kernel)
   if (t == 0 && i0 >= 0) ehat[perm[i0]] ^= 1;
   if (t == 0) a.status[shot] = 0;
 }
@@ -1185,12 +1187,170 @@ __device__ int first_setdiff(int n, const unsigned char* inJ, int nJ, int* table
 }
 
 const void* select_osd_kernel(int nw) {
+  if (nw <= 0) return nullptr;                      // (osd_nw_of: more than 33 words)
   if (nw <= 4) return (const void*)&osd_kernel<4>;
   if (nw <= 9) return (const void*)&osd_kernel<9>;
   if (nw <= 17) return (const void*)&osd_kernel<17>;
   if (nw <= 33) return (const void*)&osd_kernel<33>;
   return nullptr;
 }
+
+// ---------------------------------------------------------------------------
+// OSD for codes past the register / LDS kernels (m > 1024 rows, or more than
+// 33 row words: n > 2111): osd_kernel's exact-REF column protocol with the
+// working matrix in a per-shot global scratch slice (OsdHbmArgs). Thread t
+// owns the REF row positions t, t + B, ...; the current word of every row is
+// cached in LDS (cw), so the pivot search and the "holds a 1" tests never
+// touch global memory; a pivot's words w.. are staged in LDS (prow, and the
+// row it displaces in xr), and every row holding a 1 in the column XORs them
+// into its words w.. in global memory (word-major, so a word of consecutive
+// positions is contiguous). Per column: the pivot is the first position >=
+// xrow holding a 1 (REF, gf2math.py:139-187), rows below and above are
+// reduced, J and e_J as in osd_kernel (decoders.py:329-368). Two workgroup
+// barriers per pivot column, one per dependent column.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) osd_hbm_kernel(OsdArgs a, OsdHbmArgs h) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int m = a.m, n = a.n, NWr = h.nwr, MP = h.mp;
+  uint64_t* cw = (uint64_t*)lds;                       // [MP] word w of each row position
+  uint64_t* prow = cw + MP;                            // [NWr] the pivot row
+  uint64_t* xr = prow + NWr;                           // [NWr] the row the pivot displaces
+  uint64_t* emask = xr + NWr;                          // [NWr] e_I bits (decoders.py:345)
+  int* slots = (int*)(emask + NWr);                    // [2][16] per-wave candidates
+  int* misc = slots + 32;
+  const int t = threadIdx.x, B = blockDim.x, lane = t & 63, wave = t >> 6, nwaves = B >> 6;
+  const long long shot = blockIdx.x;
+  if (osd_host_shot(a, shot, n, slots)) return;
+  unsigned char* base = h.scratch + (size_t)shot * (size_t)h.stride;
+  uint64_t* R = (uint64_t*)base;
+  int* inv = (int*)(base + h.off_inv);
+  int* Jl = (int*)(base + h.off_jl);
+  unsigned char* inJ = base + h.off_inj;
+  int* table = (int*)(base + h.off_table);
+  const int32_t* perm = a.perm + shot * (long long)n;
+  const uint8_t* syn = a.syn + shot * (long long)m;
+  uint8_t* ehat = a.ehat + shot * (long long)n;
+  auto word = [&](int q, int p) -> uint64_t& { return R[(size_t)q * MP + p]; };
+
+  for (int i = t; i < n; i += B) {
+    inv[perm[i]] = i;
+    inJ[i] = 0;
+  }
+  for (size_t x = t; x < (size_t)NWr * MP; x += B) R[x] = 0;
+  __syncthreads();
+  // Hp's rows (+ the syndrome bit at column n); row r starts at position r
+  for (int r = t; r < m; r += B) {
+    for (int e = a.row_ptr[r]; e < a.row_ptr[r + 1]; ++e) {
+      const int i = inv[a.col_idx[e]];
+      word(i >> 6, r) |= 1ull << (i & 63);
+    }
+    if (syn[r] & 1) word(n >> 6, r) |= 1ull << (n & 63);
+  }
+  int xrow = 0, rank = 0, nJ = 1, step = 0;
+  bool done = a.rank == 0;                              // rank(H) = 0: IndexError below
+  if (t == 0) {
+    Jl[0] = 0;                                          // column 0 always (decoders.py:329)
+    inJ[0] = 1;
+  }
+  const int K = (m + B - 1) / B;
+  for (int w = 0; w < NWr && 64 * w < n && !done; ++w) {
+    __syncthreads();                                    // (the previous word's last pivot applied)
+    for (int p = t; p < m; p += B) cw[p] = word(w, p);
+    for (int b = 0; b < 64; ++b) {
+      const int i = 64 * w + b;
+      if (i >= n || done) break;
+      // the first position >= xrow holding a 1 in column i: per wave, the
+      // lowest hit of the lowest position round that has one
+      int cand = 0x7fffffff;
+      for (int k = 0; k < K; ++k) {
+        const int p = t + k * B;
+        const uint64_t bal = __ballot(p < m && p >= xrow && ((cw[p] >> b) & 1ull));
+        if (bal) {
+          cand = k * B + 64 * wave + __builtin_ctzll(bal);
+          break;
+        }
+      }
+      // two slot sets alternate (a wave writing set s at column k + 2 has
+      // passed column k + 1's barrier, after every read of column k's set s)
+      const int set = step & 1;
+      if (lane == 0) slots[16 * set + wave] = cand;
+      __syncthreads();
+      int piv = 0x7fffffff;
+      for (int q = 0; q < nwaves; ++q) piv = min(piv, slots[16 * set + q]);
+      ++step;
+      if (piv == 0x7fffffff) continue;                // dependent column: not in J
+      for (int q = w + t; q < NWr; q += B) {
+        prow[q] = word(q, piv);
+        xr[q] = word(q, xrow);
+      }
+      __syncthreads();
+      // the pivot row moves to position xrow (REF's swap; the row it
+      // displaces has a 0 in column i), every other row holding a 1 in
+      // column i takes it, below and above (rows at positions >= xrow are 0
+      // left of column i, and so is the pivot row: words < w never change)
+      for (int p = t; p < m; p += B) {
+        const uint64_t c = cw[p];
+        if (p == piv && piv != xrow) {
+          for (int q = w; q < NWr; ++q) word(q, p) = xr[q];
+          cw[p] = xr[w];
+        } else if (p == xrow) {
+          for (int q = w; q < NWr; ++q) word(q, p) = prow[q];
+          cw[p] = prow[w];
+        } else if ((c >> b) & 1ull) {
+          for (int q = w; q < NWr; ++q) word(q, p) ^= prow[q];
+          cw[p] = c ^ prow[w];
+        }
+      }
+      if (i != 0) {
+        if (t == 0) {
+          Jl[nJ] = i;
+          inJ[i] = 1;
+        }
+        ++nJ;
+      }
+      ++xrow;
+      ++rank;
+      if (rank >= a.rank || xrow >= m) done = true;
+      if (i == 0 && done) rank = -1;                  // column 0 alone reaches rank(H): the
+    }                                                 // greedy loop never breaks (:333-342)
+  }
+  if (rank < a.rank) {                                // greedy loop runs past column n-1
+    if (t == 0) a.status[shot] = 1;                   // (the reference raises IndexError)
+    return;
+  }
+  __syncthreads();
+  // information-set values e_I (e_perm = e_hat[perm], decoders.py:345)
+  for (int i0w = 64 * wave; i0w < 64 * NWr; i0w += B) {
+    const int i = i0w + lane;
+    const bool bit = i < n && !inJ[i] && (ehat[perm[i]] & 1);
+    const uint64_t bits = __ballot(bit);
+    if (lane == 0) emask[i0w >> 6] = bits;
+  }
+  if (t == 0) {
+    int i0 = -1;
+    if (a.order == 1 && nJ < n) i0 = first_setdiff(n, inJ, nJ, table);   // (decoders.py:344)
+    misc[2] = i0;
+  }
+  __syncthreads();
+  const int i0 = misc[2];
+  if (t == 0 && i0 >= 0) emask[i0 >> 6] ^= 1ull << (i0 & 63);  // order-1 flip (:349-350)
+  __syncthreads();
+  // e_J = (T sJ)[:|J|], T sJ = T s + R[:, I] e_I (mod 2)   (decoders.py:352-358)
+  for (int p = t; p < nJ && p < m; p += B) {
+    uint64_t acc = (word(n >> 6, p) >> (n & 63)) & 1ull;   // T s (augmented column)
+    for (int q = 0; q < NWr; ++q) acc ^= (uint64_t)(__builtin_popcountll(word(q, p) & emask[q]) & 1);
+    ehat[perm[Jl[p]]] = (uint8_t)(acc & 1ull);            // e_hat[perm] = ... (:368)
+  }
+  // an all-zero column 0 with rank(H) = m: J holds m + 1 entries, one more
+  // than T sJ has rows (the reference's assignment fails to broadcast); the
+  // host OSD writes 0 there, and so does this kernel
+  if (t == 0)
+    for (int p = m; p < nJ; ++p) ehat[perm[Jl[p]]] = 0;
+  if (t == 0 && i0 >= 0) ehat[perm[i0]] ^= 1;
+  if (t == 0) a.status[shot] = 0;
+}
+
+const void* osd_hbm_kernel_ptr() { return (const void*)&osd_hbm_kernel; }
 
 template <int NW>
 static const void* osd_block_by_rows(int m, int* rt) {
@@ -1203,6 +1363,7 @@ static const void* osd_block_by_rows(int m, int* rt) {
 // block kernel configurations whose state fits the VGPR budget without
 // spills (m <= 512 rows, n <= 1087 columns); null -> osd_kernel
 const void* select_osd_block_kernel(int nw, int m, int* rows_per_thread) {
+  if (nw <= 0) return nullptr;
   if (nw <= 4) return osd_block_by_rows<4>(m, rows_per_thread);
   if (nw <= 9) return osd_block_by_rows<9>(m, rows_per_thread);
   if (nw <= 17) return osd_block_by_rows<17>(m, rows_per_thread);

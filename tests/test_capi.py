@@ -37,7 +37,7 @@ def test_library_options_roundtrip_and_unknown_names():
     unknown name (the library itself never reads the environment)."""
     defaults = {"force_hbm": 0, "flood_generic": 0, "layered_generic": 0, "ms_lanes_per_check": 0, "bp_wave": 0,
                 "bp_lg": 1, "bp_team_w": 0, "static_sched": 0, "waves_per_wg": 0, "wg_per_cu": 0,
-                "osd_column": 0, "osd_tickets": 1, "osd_prof": 0}
+                "osd_column": 0, "osd_tickets": 1, "osd_prof": 0, "osd_hbm": 0}
     for k, v in defaults.items():
         assert _lib.get_option(k) == v, k
     with _lib.options(force_hbm=1, bp_team_w=8):

@@ -432,25 +432,129 @@ def test_device_osd_pipeline_matches_reference_at_configs3(order, device_min, os
         assert fallback == 0, (fallback, n_osd)            # the device order is NumPy's
 
 
-def test_gpu_osd_refuses_large_code_fast():
-    """A code past the GPU OSD's limits (m > 1024) is refused with
-    NotImplementedError before the host builds its rank / column bit-vectors
-    (a 3000 x 6000 H: the refusal must not pay an O(m n^2 / 64) host rank)."""
-    import time
+def test_gpu_osd_large_code_runs_on_device():
+    """A 3000 x 6000 H (past the register / LDS OSD kernels, which refused it
+    before this round) runs on the device (osd_hbm_kernel) and equals the
+    host C++ OSD shot for shot."""
     import torch
-    from qldpcsim_amd import _lib
+    from qldpcsim_amd import _lib, decoders
     rng = np.random.default_rng(8)
     m, n = 3000, 6000
     H = np.zeros((m, n), np.uint8)
     H[rng.integers(0, m, 6 * n), np.repeat(np.arange(n), 6)] = 1
     code = _lib.code_for(H, 0)
     k = 4
+    err = (rng.random((k, n)) < 0.02).astype(np.int64)
+    syn = ((err @ H.T.astype(np.int64)) % 2).astype(np.uint8)
+    post = rng.normal(0, 3, (k, n))
+    e0 = (post < 0).astype(np.uint8)
     d = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a, dt), device="cuda")  # noqa: E731
-    syn, e = d(np.zeros((k, m)), np.uint8), d(np.zeros((k, n)), np.uint8)
+    s_d, e_d = d(syn, np.uint8), d(e0, np.uint8)
     st = torch.empty(k, dtype=torch.int32, device="cuda")
-    perm = torch.arange(n, dtype=torch.int32, device="cuda").repeat(k, 1)   # a valid order, should it run
-    t0 = time.perf_counter()
-    with pytest.raises(NotImplementedError):
-        _lib.check(_lib.lib.qldpc_osd_device(code.handle, k, syn.data_ptr(), perm.data_ptr(), 0, e.data_ptr(),
-                                             st.data_ptr(), None))
-    assert time.perf_counter() - t0 < 0.5
+    perm = d(decoders.osd_perms(post), np.int32)
+    _lib.check(_lib.lib.qldpc_osd_device(code.handle, k, s_d.data_ptr(), perm.data_ptr(), 0, e_d.data_ptr(),
+                                         st.data_ptr(), None))
+    torch.cuda.synchronize()
+    want, rc = _host_osd(H, syn, e0, post, 0)
+    assert rc == 0 and np.all(st.cpu().numpy() == 0)
+    np.testing.assert_array_equal(e_d.cpu().numpy(), want)
+
+
+def _host_osd(H, syn, e0, post, order):
+    from qldpcsim_amd import _lib, decoders
+    want = np.ascontiguousarray(e0, np.uint8).copy()
+    perms = np.ascontiguousarray(decoders.osd_perms(post), np.int32)
+    code_h = _lib.code_for(H)
+    rc = _lib.lib.qldpc_osd_decode_batch(code_h.handle, len(e0), _lib.ptr(np.ascontiguousarray(syn, np.uint8)),
+                                         _lib.ptr(perms), order, _lib.ptr(want), 0)
+    return want, rc
+
+
+def _random_sparse_code(m, n, row_w, seed):
+    rng = np.random.default_rng(seed)
+    H = np.zeros((m, n), np.uint8)
+    for r in range(m):
+        H[r, rng.choice(n, row_w, replace=False)] = 1
+    return H
+
+
+@pytest.mark.parametrize("code", ["steane", "LP04_0", "LP118_2", "bicycle"])
+def test_hbm_osd_kernel_matches_default_and_host(code, qopt):
+    """osd_hbm_kernel (forced with option osd_hbm on codes the register / LDS
+    kernels also take): the same estimates and statuses as the default device
+    path and the host C++ OSD, orders 0, 1 and 2, consistent and random
+    syndromes."""
+    from qldpcsim_amd import codes
+    Hx, _ = codes.load_code(code)
+    rng = np.random.default_rng(21)
+    k = 64
+    syn = rng.integers(0, 2, (k, Hx.shape[0])).astype(np.uint8)
+    err = (rng.random((k // 2, Hx.shape[1])) < 0.06).astype(np.int64)
+    syn[: k // 2] = (err @ Hx.T.astype(np.int64)) % 2
+    post = rng.normal(0, 3, (k, Hx.shape[1]))
+    e0 = (post < 0).astype(np.uint8)
+    for order in (0, 1, 2):
+        dflt, sd = _gpu_osd(Hx, syn, e0, post, order)
+        qopt(osd_hbm=1)
+        hbm, sh = _gpu_osd(Hx, syn, e0, post, order)
+        qopt(osd_hbm=0)
+        np.testing.assert_array_equal(sh, sd)
+        np.testing.assert_array_equal(hbm, dflt)
+        ok = sd == 0
+        want, _ = _host_osd(Hx[:, :], syn[ok], e0[ok], post[ok], order)
+        np.testing.assert_array_equal(hbm[ok], want)
+
+
+@pytest.mark.parametrize("m,n", [(1100, 2300), (600, 2400), (1200, 1500)])
+def test_hbm_osd_codes_past_the_register_kernels(m, n):
+    """Codes past the register / LDS OSD kernels (m > 1024 rows or n > 2111
+    columns; before, m > 1024 was refused and n > 2111 selected a kernel too
+    narrow for the row): the device OSD equals the host C++ OSD shot for
+    shot, orders 0 and 1, consistent syndromes and random ones (status 1 where
+    the reference raises IndexError). The random codes have all-zero columns
+    (~13 % at 600 x 2400): with one first in the order and rank(H) = m, J
+    holds m + 1 entries — the reference's assignment fails to broadcast, the
+    host and device OSD both write 0 at the extra entry."""
+    H = _random_sparse_code(m, n, 8, m + n)
+    rng = np.random.default_rng(m * 7 + n)
+    k = 24
+    syn = rng.integers(0, 2, (k, m)).astype(np.uint8)
+    err = (rng.random((k // 2, n)) < 0.03).astype(np.int64)
+    syn[: k // 2] = (err @ H.T.astype(np.int64)) % 2
+    post = rng.normal(0, 3, (k, n))
+    e0 = (post < 0).astype(np.uint8)
+    for order in (0, 1):
+        got, st = _gpu_osd(H, syn, e0, post, order)
+        assert np.all(st[: k // 2] == 0), st
+        for i in range(k):
+            want, rc = _host_osd(H, syn[i:i + 1], e0[i:i + 1], post[i:i + 1], order)
+            if st[i] == 0:
+                assert rc == 0
+                np.testing.assert_array_equal(got[i], want[0], err_msg=f"shot {i} order {order}")
+            else:
+                assert st[i] == 1 and rc != 0                      # both: the reference's IndexError
+                np.testing.assert_array_equal(got[i], e0[i])      # e_hat left unchanged
+
+
+@pytest.mark.parametrize("m,n", [(1100, 1800), (700, 2300)])
+def test_apply_osd_device_on_codes_past_the_register_kernels(m, n, osdpol):
+    """The pipeline's own entry (apply_osd_device: device order where n <=
+    2048, NumPy's order on the host past it, then the device elimination) on
+    codes past the register / LDS OSD kernels equals the host OSD."""
+    import torch
+    from qldpcsim_amd import decoders
+    H = _random_sparse_code(m, n, 8, 3 * m + n)
+    rng = np.random.default_rng(m + 5 * n)
+    k = 16
+    err = (rng.random((k, n)) < 0.03).astype(np.int64)
+    syn = ((err @ H.T.astype(np.int64)) % 2).astype(np.uint8)
+    post = rng.normal(0, 3, (k, n))
+    e0 = (post < 0).astype(np.uint8)
+    want, rc = _host_osd(H, syn, e0, post, 0)
+    assert rc == 0
+    osdpol(device_min=1)
+    d = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a, dt), device="cuda")  # noqa: E731
+    res = decoders.DecodeResult(d(e0, np.uint8), torch.zeros(k, dtype=torch.int32, device="cuda"),
+                                d(post, np.float64), torch.zeros(k, dtype=torch.int32, device="cuda"))
+    decoders.apply_osd_device(H, d(syn, np.uint8), res, 0)
+    np.testing.assert_array_equal(res.ehat.cpu().numpy(), want)
