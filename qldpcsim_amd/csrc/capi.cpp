@@ -322,6 +322,7 @@ struct LaunchCfg {
   bool tlg = false;      // bp_team_lg_kernel: every table global, LDS image = layer pointers
   bool hbm = false;      // the LDS kernels cannot hold this schedule: hbm_tile_kernel (cached)
   int msl_gt = 0;        // ms_layered_kernel<DC, 1> built with QLDPC_MSL_GT: tables left in global memory
+  int synl_rows = 0;     // ms_layered_kernel<DC, 0>: layer-ordered syndrome bits per wave (rows)
   uint32_t gen = 0;      // g_opt.gen the configuration was built under
   int team = 0;          // bp_team_kernel: waves per half-shot (one workgroup), 0 = wave kernels
   const char* name = "";  // kernel name as rocprofv3 reports it
@@ -689,8 +690,11 @@ extern "C" int qldpc_schedule_release_workspace(qldpc_schedule* s) {
 }
 
 // per-wave state slice: post f64[n] | c2v (f32|f64)[E] | syn words | parity words
+// (ms_layered_kernel, colsum_f32: the "parity words" slot holds the syndrome
+// bits in layer order instead, 2 ceil(synl_rows / 64) words; the lane-group
+// instance <DC, 0> only)
 static void wave_layout(const qldpc_code* c, bool layered, int algo, int* bytes, int* off_c2v,
-                        int* off_synw, int* off_parw, bool colsum_f32 = false) {
+                        int* off_synw, int* off_parw, bool colsum_f32 = false, int synl_rows = 0) {
   int off = align16((colsum_f32 ? 4 : 8) * c->n);   // post f64, or ms_layered_kernel's float32 sums
   *off_c2v = off;
   off = align16(off + (algo == QLDPC_ALGO_MS ? 4 : 8) * (c->E + 8));  // +8: VN over-read pad
@@ -698,7 +702,8 @@ static void wave_layout(const qldpc_code* c, bool layered, int algo, int* bytes,
   *off_synw = off;
   if (layered) off = align16(off + 4 * words);
   *off_parw = off;
-  if (layered && !colsum_f32) off = align16(off + 4 * words);  // ms_layered_kernel: filters, no parity words
+  if (layered && !colsum_f32) off = align16(off + 4 * words);
+  if (layered && colsum_f32) off = align16(off + 4 * 2 * ((synl_rows + 63) / 64));
   *bytes = std::max(off, 16);
 }
 
@@ -759,6 +764,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg* out) {
     cfg.kernel = qldpc::select_ms_layered_kernel(dc, g, &cfg.name);
     use_lblob = cfg.kernel != nullptr;
     cfg.msl_gt = use_lblob && g == 1 && s->l_off_ltab == 0 ? QLDPC_MSL_GT : 0;
+    cfg.synl_rows = use_lblob && g == 0 ? (int)s->h_lay_rows.size() : 0;
   }
   cfg.lblob = use_lblob;
   cfg.gtab = gtab;
@@ -789,7 +795,7 @@ static int launch_config(qldpc_schedule* s, int algo, LaunchCfg* out) {
   cfg.team = team;
   if (!cfg.kernel) cfg.kernel = qldpc::select_kernel(algo, s->layered, dc, &cfg.name);
   int off_c2v, off_synw, off_parw, off_red;
-  wave_layout(c, s->layered, algo, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw, use_lblob);
+  wave_layout(c, s->layered, algo, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw, use_lblob, cfg.synl_rows);
   if (team) team_layout(c, team, &cfg.wave_bytes, &off_c2v, &off_synw, &off_parw, &off_red);
   int max_lds = 0, dev = 0;
   HIP_TRY(hipGetDevice(&dev));
@@ -1091,7 +1097,8 @@ extern "C" int qldpc_decode_device_ex(const qldpc_code* code, const qldpc_schedu
   a.off_adj_ptr = sched->off_adj_ptr;
   a.off_adj_vars = sched->off_adj_vars;
   a.off_chunk_dmax = sched->off_chunk_dmax;
-  wave_layout(code, sched->layered, algo, &a.wave_bytes, &a.off_c2v, &a.off_synw, &a.off_parw, cfg->lblob);
+  wave_layout(code, sched->layered, algo, &a.wave_bytes, &a.off_c2v, &a.off_synw, &a.off_parw, cfg->lblob,
+              cfg->synl_rows);
   if (cfg->lblob) {  // ms_layered_kernel's blob: field mapping documented in the kernel
     a.blob = sched->d_lblob;
     a.blob_bytes = (int)sched->lblob.size();

@@ -1526,9 +1526,12 @@ __device__ __forceinline__ bool layered_full_check(const DecodeArgs& a, const fl
 // lanes per check: GG = 1 walks a row's DC edges in one lane (cn_ms_compute),
 // GG > 1 splits them over a lane group (cn_ms_split). All rows read the same
 // snapshot of the column sums (Jacobi within the layer, decoders.py:155-169).
-template <int DC, int GG, bool UNI = false>
+// SYNL: the syndrome bit by layer position (synl[q]), else by check index
+// (lrow[q], then synw) — see the synl build in ms_layered_kernel
+template <int DC, int GG, bool UNI = false, bool SYNL = false>
 __device__ __forceinline__ void cn_layer(const DecodeArgs& a, const uint32_t* ltab, const uint16_t* lrow,
-                                         const uint32_t* synw, int q0, int q1, int lane, bool first,
+                                         const uint32_t* synw, const uint32_t* synl, int q0, int q1, int lane,
+                                         bool first,
                                          const float* colS, unsigned char* c2v_b, uint32_t post_b,
                                          uint32_t c2v_a, int& fl) {
   if constexpr (GG == 1) {
@@ -1542,7 +1545,8 @@ __device__ __forceinline__ void cn_layer(const DecodeArgs& a, const uint32_t* lt
       const int q = !UNI ? qi : min(qi + lane, q1 - 1);
       uint32_t t[1][8];
       load_row8(ltab + q * 8, t[0]);
-      const int c = lrow[q];
+      const int c = SYNL ? q : lrow[q];
+      const uint32_t* sw_base = SYNL ? synl : synw;
       // The row words and the check index go out in one LDS round trip, and
       // the syndrome word with the messages: left alone, the compiler waited
       // for the index before issuing the row reads and hoisted the syndrome
@@ -1551,7 +1555,7 @@ __device__ __forceinline__ void cn_layer(const DecodeArgs& a, const uint32_t* lt
       __builtin_amdgcn_sched_barrier(0);
       const bool live[1] = {true};
       if (first) {
-        const uint32_t sb[1] = {(synw[c >> 5] >> (c & 31)) & 1u};
+        const uint32_t sb[1] = {(sw_base[c >> 5] >> (c & 31)) & 1u};
         (void)cn_ms_uniform<DC, true, 1>(a, t, sb, live, (const unsigned char*)colS, c2v_b, fl);
       } else {
         CnLoad<DC> Ld;
@@ -1565,7 +1569,7 @@ __device__ __forceinline__ void cn_layer(const DecodeArgs& a, const uint32_t* lt
         }
         // every read issued before any arithmetic (left alone, the scheduler
         // split the 16 reads over three round trips)
-        uint32_t sw = synw[c >> 5];
+        uint32_t sw = sw_base[c >> 5];
 #pragma unroll
         for (int k = 0; k < DC; ++k) asm volatile("" : "+v"(pf[k]), "+v"(Ld.cv[k]));
         asm volatile("" : "+v"(sw));
@@ -1581,8 +1585,8 @@ __device__ __forceinline__ void cn_layer(const DecodeArgs& a, const uint32_t* lt
       const int q = qb + lane / GG;
       const bool live = q < q1;
       const int qs = live ? q : q0;
-      const int c = lrow[qs];
-      const uint32_t sb = (synw[c >> 5] >> (c & 31)) & 1u;
+      const int c = SYNL ? qs : lrow[qs];
+      const uint32_t sb = ((SYNL ? synl : synw)[c >> 5] >> (c & 31)) & 1u;
       cn_ms_split<DC, GG>(a, ltab + qs * 8, lane & (GG - 1), live, sb, first, post_b, c2v_a, fl);
     }
   }
@@ -1639,6 +1643,7 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
   unsigned char* c2v_b = ws + a.off_c2v;
   float* c2v = (float*)c2v_b;
   uint32_t* synw = (uint32_t*)(ws + a.off_synw);
+  uint32_t* synl = (uint32_t*)(ws + a.off_parw);                      // syndrome bits by layer position
   const uint32_t post_b = lds_addr(colS), c2v_a = lds_addr(c2v_b);
   const int m = a.m, n = a.n;
   const float thr = a.hd_thresh;
@@ -1670,6 +1675,26 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
       load_syndrome_bits<8>(ak, hs, synw, lane);
       for (int j = lane; j < n; j += 64) colS[j] = 0.0f;          // post = L, c2v = 0 (:148-150)
       for (int p = lane; p < ak.E; p += 64) c2v[p] = 0.0f;
+    }
+    wave_sync();
+    if constexpr (G == 0) {
+      // the syndrome bits in layer order, once per half-shot (the per-layer
+      // lane-group instance): each check node reads its bit by layer
+      // position (synl) instead of the check index and then the syndrome
+      // word: LP118_0 layered 55.08 -> 54.27 ms per launch; the one-lane
+      // instance measured slower with it (LP118_2 p = 0.1 +0.9 %, p = 0.05
+      // +2.3 %: the index read hides under the row words' global load, the
+      // per-half-shot build does not), profiles/r06/r06y_ab_synl.json
+      const int nq = lay_ptr[a.n_layers];
+      for (int qb = 0; qb < nq; qb += 64) {
+        const int q = qb + lane;
+        const int c = q < nq ? lrow[q] : 0;
+        const uint64_t bl = ballot(q < nq && ((synw[c >> 5] >> (c & 31)) & 1u));
+        if (lane == 0) {
+          synl[qb >> 5] = (uint32_t)bl;
+          synl[(qb >> 5) + 1] = (uint32_t)(bl >> 32);
+        }
+      }
     }
     wave_sync();
     // filter parities of the syndrome (B) and of the hard decisions (F: all
@@ -1715,16 +1740,16 @@ __global__ void __launch_bounds__(QLDPC_MAX_THREADS) ms_layered_kernel(DecodeArg
               cn_ms_pair_uni(a, ltab + qs * 8, lane & 1, sb, first, post_b, c2v_a, fl);
             }
           } else
-            cn_layer<DC, G, G == 1>(a, ltab, lrow, synw, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl);
+            cn_layer<DC, G, G == 1>(a, ltab, lrow, synw, synl, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl);
           if constexpr (QLDPC_MSL_PRIO == 1) __builtin_amdgcn_s_setprio(0);
           if constexpr (QLDPC_MSL_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         } else {
           // lanes per check chosen per layer by the host (bits 5-6 of adj_dmax)
           switch ((dsel >> 5) & 3) {
-            case 0: cn_layer<DC, 1>(a, ltab, lrow, synw, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl); break;
-            case 1: cn_layer<DC, 2>(a, ltab, lrow, synw, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl); break;
-            case 2: cn_layer<DC, 4>(a, ltab, lrow, synw, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl); break;
-            default: cn_layer<DC, 8>(a, ltab, lrow, synw, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl); break;
+            case 0: cn_layer<DC, 1, false, true>(a, ltab, lrow, synw, synl, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl); break;
+            case 1: cn_layer<DC, 2, false, true>(a, ltab, lrow, synw, synl, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl); break;
+            case 2: cn_layer<DC, 4, false, true>(a, ltab, lrow, synw, synl, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl); break;
+            default: cn_layer<DC, 8, false, true>(a, ltab, lrow, synw, synl, q0, q1, lane, first, colS, c2v_b, post_b, c2v_a, fl); break;
           }
         }
         first = false;
