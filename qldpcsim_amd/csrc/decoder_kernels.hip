@@ -1437,6 +1437,16 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
 // TWO (round 6): every degree is LO or K (bit 8; LP118_2's 3 / 5): one select
 // of the two prefix sums (32.42 -> 31.71 ms per LP118_2 p = 0.1 launch,
 // profiles/r06/r06h_ab_msl_two_min.json)
+// one IEEE float32 add (round to nearest, the same v_add_f32 the compiler
+// emits) that the SLP vectorizer cannot pair into v_pk_add_f32: the paired
+// prefix sums of two variables needed a register move per pair to line up
+// their operands (-0.8 % per LP118_2 p = 0.1 launch,
+// profiles/r06/r06aa_ab_vn_asm_add.json)
+__device__ __forceinline__ float vadd_f32(float a, float b) {
+  float r;
+  asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 template <int K, int H, int LO = 1, bool TWO = false>
 __device__ __forceinline__ uint32_t vn_layer(const uint32_t* adj_info, const uint32_t* avar, float* colS,
                                              const float* c2v, int v0, int v1, int lane, float thr) {
@@ -1468,13 +1478,13 @@ __device__ __forceinline__ uint32_t vn_layer(const uint32_t* adj_info, const uin
       const int d = (int)((info[h] >> 16) & 31u);
       float s = 0.0f;                                       // sequential, ascending check (:172)
       if constexpr (LO > 1) {
-        float pre = 0.0f + x[h][0];
+        float pre = vadd_f32(0.0f, x[h][0]);
 #pragma unroll
-        for (int t = 1; t < LO; ++t) pre += x[h][t];
+        for (int t = 1; t < LO; ++t) pre = vadd_f32(pre, x[h][t]);
         s = pre;                                            // d = LO
 #pragma unroll
         for (int t = LO; t < K; ++t) {
-          pre += x[h][t];                                   // (slots past d: discarded below)
+          pre = vadd_f32(pre, x[h][t]);                     // (slots past d: discarded below)
           if constexpr (!TWO) s = d > t ? pre : s;
         }
         if constexpr (TWO) s = d > LO ? pre : s;            // every degree is LO or K
