@@ -35,10 +35,12 @@ B=qldpcsim_amd/_build
 
 declare -A CFG=(
   [flood]=""
+  [msl2p01]="--code LP118_2 --schedule L --p 0.01 --batch 1048576"
   [msl2p05]="--code LP118_2 --schedule L --p 0.05 --batch 262144"
   [msl2p10]="--code LP118_2 --schedule L --p 0.1 --batch 131072"
   [msl0]="--schedule L --batch 262144"
   [bpl2p10]="--code LP118_2 --algo BP --schedule L --iters 100 --p 0.1 --batch 65536"
+  [bpl2p01]="--code LP118_2 --algo BP --schedule L --iters 100 --p 0.01 --batch 524288"
   [bpl2p05]="--code LP118_2 --algo BP --schedule L --iters 100 --p 0.05 --batch 131072"
   [bpf0]="--algo BP --iters 100 --batch 65536"
   [hbm]="--path hbm --batch 262144 --hbm-leg 0"
